@@ -1,0 +1,114 @@
+/*
+ * tq.h -- C ABI of the MI355X term-quantization (TQ) library, libtq_hip.so.
+ *
+ * The drop-in boundary for the reference's one native op and the accumulation it leaves to
+ * cuDNN.  Plain pointers and sizes only; every pointer argument except `stream` is a
+ * device pointer (HIP), and work is enqueued on `stream` (a hipStream_t of the calling
+ * thread's current device; NULL = the null stream).  Calls are asynchronous, keep no global
+ * mutable state and are safe to issue from several host threads.
+ *
+ * Every entry point returns TQ_OK (0) or a TQ_ERR_* code; tq_last_error() then returns a
+ * message for the calling thread.  The Python host layer (term-quantization_amd/tq_native.py)
+ * raises RuntimeError with that message, as the reference's AT_ASSERTM checks do
+ * (kernels/tr_cuda.cpp:12-18).  Python binding: INTEGRATION.md.
+ */
+#ifndef TQ_H_
+#define TQ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  TQ_OK = 0,
+  TQ_ERR_INVALID_ARGUMENT = 1, /* shape / parameter outside the contract */
+  TQ_ERR_UNSUPPORTED = 2,      /* inside the reference's domain but not implemented */
+  TQ_ERR_HIP = 3               /* a HIP runtime error (launch or memset) */
+};
+
+/* Library version string, e.g. "tq-hip 0.1.0 gfx950". */
+const char *tq_version(void);
+
+/* Message for the last non-OK return on the calling thread ("" if none). */
+const char *tq_last_error(void);
+
+/*
+ * Term-revealing op, float32 / float64.  Replaces the pybind entry
+ *   at::Tensor tr(const at::Tensor input, const float sf, const int32_t bitwidth,
+ *                 const int32_t group_size, const int32_t num_keep_terms)
+ * of kernels/tr_cuda.cpp:20-24 and its launcher tr_cuda (kernels/tr_cuda_kernel.cu:128-160).
+ *
+ * `input` is a contiguous tensor of `ndim` >= 2 dims with sizes `shape`; `output` has the
+ * same shape and receives sf * (sum of the kept HESE terms) per element.  As in the
+ * reference, B = shape[0], C = shape[1], W,H = shape[2],shape[3] for 4-D inputs and 1
+ * otherwise; a group is `group_size` consecutive channels at one (b, w, h); the first
+ * `num_keep_terms` terms of each group in (exponent desc, channel asc) order are kept;
+ * elements past B*C*W*H (3-D / 5-D inputs) are written as 0.
+ * Domain: 0 <= bitwidth <= 24, 1 <= group_size <= 32, sf >= 0 (+inf allowed), ndim >= 2.
+ * C % group_size != 0 uses a partial last group (the reference races there).
+ */
+int tq_tr_f32(const float *input, float *output, int64_t ndim, const int64_t *shape, float sf,
+              int32_t bitwidth, int32_t group_size, int32_t num_keep_terms, void *stream);
+int tq_tr_f64(const double *input, double *output, int64_t ndim, const int64_t *shape,
+              float sf, int32_t bitwidth, int32_t group_size, int32_t num_keep_terms,
+              void *stream);
+
+/*
+ * tq_tr_f32 that also writes the integer term sums: codes[i] = v with output[i] = v * sf
+ * (|v| <= 2^bitwidth).  Used once per layer to pre-encode weights for the term-pair
+ * kernels (the weight call of tr_layer.py:117-121).
+ */
+int tq_tr_encode_f32(const float *input, float *output, int32_t *codes, int64_t ndim,
+                     const int64_t *shape, float sf, int32_t bitwidth, int32_t group_size,
+                     int32_t num_keep_terms, void *stream);
+
+/*
+ * Activation TR (group_size 1, tr_layer.py:96-99) from fp32 straight into int16 term-sum
+ * codes in NHWC with `cp` channels per pixel (cp % 8 == 0, cp >= c, pad channels = 0).
+ * `in_nhwc` = 1 for a channels_last input, 0 for NCHW.  Domain: 0 <= bitwidth <= 14.
+ */
+int tq_act_encode(const float *x, int32_t in_nhwc, int64_t n, int64_t c, int64_t h, int64_t w,
+                  float sf, int32_t bitwidth, int32_t num_keep_terms, int16_t *codes,
+                  int64_t cp, void *stream);
+
+/* Rows the weight-code matrix of tq_conv2d_termpair must be padded to (a multiple of). */
+int64_t tq_conv2d_cout_align(void);
+
+/*
+ * Term-pair Conv2d (groups = 1): the exact integer sum over (kh, kw, c) of
+ * act_codes * w_codes per output, scaled once: out = fp32(acc * scale) + bias.
+ * With scale = double(sf_x) * double(sf_w) this is conv2d(TR(x), TR(w)) + bias -- the
+ * reference's `self.conv(xq)` (tr_layer.py:124-126) on its fake-quantized tensors, to
+ * within one fp32 rounding of the exact result.
+ *   act_codes  [n][h][w][cp] int16 (tq_act_encode), 16-byte aligned
+ *   w_codes    [cout_pad][kp] int16, k = (i*kw + j)*cp + c; cout_pad a multiple of
+ *              tq_conv2d_cout_align(), kp a multiple of 32, padding zero
+ *   bias       [cout] float or NULL
+ *   out        float, [n][cout][ho][wo] (out_nhwc = 0) or [n][ho][wo][cout] (out_nhwc = 1)
+ * The caller guarantees the int32 accumulator cannot overflow
+ * (max_o sum_k |w_codes[o][k]| * max|act_code| < 2^31).
+ */
+int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w, int64_t cp,
+                       const int16_t *w_codes, int64_t cout, int64_t kh, int64_t kw, int64_t kp,
+                       int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                       int64_t dil_h, int64_t dil_w, double scale, const float *bias,
+                       float *out, int64_t ho, int64_t wo, int32_t out_nhwc, void *stream);
+
+/*
+ * Batched activation-scale calibration, replacing the 2048-launch loop of
+ * tr_layer.mse_profile (tr_layer.py:43-54):
+ *   errs[s] = sum_b hist[b] * (x[b] - TR(x[b]; sf = sfs[s], bitwidth, group 1, k))^2
+ * for s < nsf, the per-bin term in fp32 as the reference's torch expression, the sum over
+ * bins in fp64.  The caller takes the first arg-min (torch.argmin semantics).
+ */
+int tq_mse_profile(const float *x, const float *hist, int64_t nbins, const float *sfs,
+                   int64_t nsf, int32_t bitwidth, int32_t num_keep_terms, double *errs,
+                   void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TQ_H_ */

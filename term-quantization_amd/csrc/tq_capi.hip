@@ -1,0 +1,182 @@
+// C-ABI entry points of libtq_hip.so (declared in include/tq.h).  Argument validation
+// lives here so every kernel can assume its contract; nothing here allocates or syncs, so
+// the calls are capturable in a hipGraph.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "../../include/tq.h"
+#include "tq_device.h"
+#include "tq_launch.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return TQ_OK;
+  return fail(TQ_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+int check_tr_args(int64_t ndim, const int64_t* shape, float sf, int32_t bitwidth,
+                  int32_t group_size, int64_t* B, int64_t* C, int64_t* WH, int64_t* numel) {
+  if (ndim < 2 || shape == nullptr)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "tr: input must have at least 2 dimensions (got %lld)",
+                (long long)ndim);
+  int64_t n = 1;
+  for (int64_t d = 0; d < ndim; ++d) {
+    if (shape[d] < 0) return fail(TQ_ERR_INVALID_ARGUMENT, "tr: negative size");
+    n *= shape[d];
+  }
+  if (!(sf >= 0.0f))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "tr: sf must be >= 0 (got %g)", (double)sf);
+  if (bitwidth < 0 || bitwidth > tq::kMaxBitwidth)
+    return fail(TQ_ERR_UNSUPPORTED, "tr: bitwidth must be in [0, %d] (got %d)",
+                tq::kMaxBitwidth, bitwidth);
+  if (group_size < 1 || group_size > 32)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "tr: group_size must be in [1, 32] (got %d)",
+                group_size);
+  *B = shape[0];
+  *C = shape[1];
+  *WH = ndim == 4 ? shape[2] * shape[3] : 1;  // kernels/tr_cuda_kernel.cu:133-141
+  *numel = n;
+  return TQ_OK;
+}
+
+template <typename T>
+int tr_impl(const T* in, T* out, int32_t* codes, int64_t ndim, const int64_t* shape, float sf,
+            int32_t bitwidth, int32_t group_size, int32_t k, void* stream) {
+  int64_t B, C, WH, numel;
+  int rc = check_tr_args(ndim, shape, sf, bitwidth, group_size, &B, &C, &WH, &numel);
+  if (rc != TQ_OK) return rc;
+  if (numel == 0) return TQ_OK;
+  if (in == nullptr || out == nullptr)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "tr: null tensor pointer");
+  // num_keep_terms < 0 runs no selection step in the reference: nothing is kept.
+  const int kk = k < 0 ? 0 : k;
+  return hip_status(tq::launch_tr<T>(in, out, codes, B, C, WH, numel, sf, bitwidth, group_size,
+                                     kk, (hipStream_t)stream),
+                    "tr launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tq_version(void) { return "tq-hip 0.1.0 gfx950"; }
+
+const char* tq_last_error(void) { return g_err; }
+
+int tq_tr_f32(const float* input, float* output, int64_t ndim, const int64_t* shape, float sf,
+              int32_t bitwidth, int32_t group_size, int32_t num_keep_terms, void* stream) {
+  return tr_impl<float>(input, output, nullptr, ndim, shape, sf, bitwidth, group_size,
+                        num_keep_terms, stream);
+}
+
+int tq_tr_f64(const double* input, double* output, int64_t ndim, const int64_t* shape,
+              float sf, int32_t bitwidth, int32_t group_size, int32_t num_keep_terms,
+              void* stream) {
+  return tr_impl<double>(input, output, nullptr, ndim, shape, sf, bitwidth, group_size,
+                         num_keep_terms, stream);
+}
+
+int tq_tr_encode_f32(const float* input, float* output, int32_t* codes, int64_t ndim,
+                     const int64_t* shape, float sf, int32_t bitwidth, int32_t group_size,
+                     int32_t num_keep_terms, void* stream) {
+  if (codes == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "tr_encode: codes is null");
+  return tr_impl<float>(input, output, codes, ndim, shape, sf, bitwidth, group_size,
+                        num_keep_terms, stream);
+}
+
+int tq_act_encode(const float* x, int32_t in_nhwc, int64_t n, int64_t c, int64_t h, int64_t w,
+                  float sf, int32_t bitwidth, int32_t num_keep_terms, int16_t* codes,
+                  int64_t cp, void* stream) {
+  if (n < 0 || c < 1 || h < 0 || w < 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: bad shape");
+  if (cp < c || cp % 8 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: cp must be >= c and a multiple of 8");
+  if (bitwidth < 0 || bitwidth > 14)
+    return fail(TQ_ERR_UNSUPPORTED, "act_encode: int16 codes need bitwidth <= 14 (got %d)",
+                bitwidth);
+  if (!(sf >= 0.0f)) return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: sf must be >= 0");
+  if ((uintptr_t)codes % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: codes must be 16-byte aligned");
+  if (in_nhwc && cp == c && (uintptr_t)x % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: x must be 16-byte aligned");
+  const int kk = num_keep_terms < 0 ? 0 : num_keep_terms;
+  return hip_status(tq::launch_act_encode(x, in_nhwc, n, c, h, w, sf, bitwidth, kk, codes, cp,
+                                          (hipStream_t)stream),
+                    "act_encode launch");
+}
+
+int64_t tq_conv2d_cout_align(void) { return 128; }
+
+int tq_conv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t cp,
+                       const int16_t* w_codes, int64_t cout, int64_t kh, int64_t kw, int64_t kp,
+                       int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                       int64_t dil_h, int64_t dil_w, double scale, const float* bias,
+                       float* out, int64_t ho, int64_t wo, int32_t out_nhwc, void* stream) {
+  if (n < 0 || h < 1 || w < 1 || cout < 1 || kh < 1 || kw < 1)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad shape");
+  if (cp < 8 || cp % 8 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: cp must be a positive multiple of 8");
+  if (kp % 32 != 0 || kp < kh * kw * cp)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: kp must be a multiple of 32 >= kh*kw*cp");
+  if (stride_h < 1 || stride_w < 1 || dil_h < 1 || dil_w < 1 || pad_h < 0 || pad_w < 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad stride/padding/dilation");
+  const int64_t eho = (h + 2 * pad_h - dil_h * (kh - 1) - 1) / stride_h + 1;
+  const int64_t ewo = (w + 2 * pad_w - dil_w * (kw - 1) - 1) / stride_w + 1;
+  if (ho != eho || wo != ewo || ho < 1 || wo < 1)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: output size %lldx%lld, expected %lldx%lld",
+                (long long)ho, (long long)wo, (long long)eho, (long long)ewo);
+  if ((uintptr_t)act_codes % 16 != 0 || (uintptr_t)w_codes % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: code buffers must be 16-byte aligned");
+  if (n * h * w * cp >= (int64_t)1 << 40 || cout > (1 << 24) || kp > (1 << 24))
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d: problem too large");
+  tq::ConvArgs a;
+  a.x = act_codes;
+  a.w = w_codes;
+  a.bias = bias;
+  a.out = out;
+  a.P = n * ho * wo;
+  a.N = (int)n;
+  a.H = (int)h;
+  a.W = (int)w;
+  a.Cp = (int)cp;
+  a.Cout = (int)cout;
+  a.KH = (int)kh;
+  a.KW = (int)kw;
+  a.sh = (int)stride_h;
+  a.sw = (int)stride_w;
+  a.ph = (int)pad_h;
+  a.pw = (int)pad_w;
+  a.dh = (int)dil_h;
+  a.dw = (int)dil_w;
+  a.Ho = (int)ho;
+  a.Wo = (int)wo;
+  a.Kp = (int)kp;
+  a.scale = scale;
+  return hip_status(tq::launch_conv2d_tp(a, out_nhwc, (hipStream_t)stream), "conv2d launch");
+}
+
+int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
+                   int64_t nsf, int32_t bitwidth, int32_t num_keep_terms, double* errs,
+                   void* stream) {
+  if (nbins < 0 || nsf < 0 || nbins > (1 << 30) || nsf > (1 << 30))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "mse_profile: bad sizes");
+  if (bitwidth < 0 || bitwidth > tq::kMaxBitwidth)
+    return fail(TQ_ERR_UNSUPPORTED, "mse_profile: bitwidth must be in [0, %d]", tq::kMaxBitwidth);
+  const int kk = num_keep_terms < 0 ? 0 : num_keep_terms;
+  return hip_status(tq::launch_mse_profile(x, hist, nbins, sfs, nsf, bitwidth, kk, errs,
+                                           (hipStream_t)stream),
+                    "mse_profile launch");
+}
+
+}  // extern "C"

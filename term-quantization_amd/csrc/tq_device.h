@@ -1,0 +1,78 @@
+// Device-side building blocks of the term-revealing (TR) path on CDNA4 (gfx950).
+//
+// Every function here restates one step of the reference kernel
+// (kernels/tr_cuda_kernel.cu) in a form that suits a 64-lane wavefront: no per-element
+// 64-slot term array, no data-dependent 64-iteration loop -- the HESE terms of an element
+// are two 32-bit masks computed in registers, and term selection works on those masks.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tq {
+
+constexpr int kMaxGroupSize = 32;  // kernels/tr_cuda_kernel.cu:9 (MAX_GROUP_SIZE)
+constexpr int kMaxBitwidth = 24;   // keeps every partial sum exact in fp32
+
+// a1 -- quantize: kernels/tr_cuda_kernel.cu:21-23.
+//   q = min(sat_int32(double(fp32(|x| / sf)) + 0.5), 2^bw - 1), NaN -> 0.
+// The +0.5 is a double add in the reference (the literal 0.5 promotes); doing it in fp32
+// rounds |x|/sf = 0.49999997f up to 1.  With maxv <= 2^24 - 1 (exact in fp32) the
+// reference's fminf(float(int), maxv) round trip equals an integer min, so clamping the
+// double before the conversion gives the same q for every input, +-inf and NaN included.
+__device__ __forceinline__ uint32_t quantize_mag(float x, float sf, float maxv) {
+  const double t = (double)(fabsf(x) / sf) + 0.5;
+  return (t == t) ? (uint32_t)fmin(t, (double)maxv) : 0u;
+}
+
+// The float64 instantiation of the reference kernel divides in double.
+__device__ __forceinline__ uint32_t quantize_mag(double x, float sf, float maxv) {
+  const double t = fabs(x) / (double)sf + 0.5;
+  return (t == t) ? (uint32_t)fmin(t, (double)maxv) : 0u;
+}
+
+// a2 -- HESE encode: kernels/tr_cuda_kernel.cu:25-55 and bit_utils.hese (bit_utils.py:10-44).
+// The reference scans bit windows (b[i+1], b[i], b[i-1]) from bit 63 down:
+//   010 -> +2^i (and skip bit i-1), 011 -> +2^(i+1), 110 -> -2^i.
+// Closed form on the whole word (checked against bit_utils.hese for every q < 2^17):
+//   P = (q & ~(q>>1) & ~(q<<1)) | ((q & ~(q>>1) & (q<<1)) << 1),  N = q & (q>>1) & ~(q<<1)
+// so q == P - N with P & N == 0: each set bit of P (N) is a +2^e (-2^e) term and all term
+// exponents are distinct.  Terms come out of the reference in strictly decreasing
+// exponent order, i.e. the order of the set bits of (P | N) from the top.
+__device__ __forceinline__ void hese_masks(uint32_t q, uint32_t& pos, uint32_t& neg) {
+  const uint32_t hi = q >> 1;
+  const uint32_t lo = q << 1;
+  const uint32_t a = q & ~hi;
+  pos = (a & ~lo) | ((a & lo) << 1);
+  neg = q & hi & ~lo;
+}
+
+// a3 for group_size == 1: the greedy of kernels/tr_cuda_kernel.cu:92-116 over a single
+// element keeps its k largest-exponent terms.  Drop the (popcount - k) lowest set bits.
+__device__ __forceinline__ uint32_t keep_top_terms(uint32_t mask, int k) {
+  int drop = __popc(mask) - k;
+  while (drop > 0) {
+    mask &= mask - 1u;
+    --drop;
+  }
+  return mask;
+}
+
+// a4 -- value of the kept terms, with the element's sign: kernels/tr_cuda_kernel.cu:112.
+__device__ __forceinline__ int32_t kept_value(uint32_t pos, uint32_t neg, uint32_t keep,
+                                              bool negative) {
+  const int32_t v = (int32_t)(pos & keep) - (int32_t)(neg & keep);
+  return negative ? -v : v;
+}
+
+// One element through quantize -> encode -> keep top k -> signed integer value.
+template <typename T>
+__device__ __forceinline__ int32_t tr_value_g1(T x, float sf, float maxv, int k) {
+  const uint32_t q = quantize_mag(x, sf, maxv);
+  uint32_t pos, neg;
+  hese_masks(q, pos, neg);
+  const uint32_t keep = keep_top_terms(pos | neg, k);
+  return kept_value(pos, neg, keep, x < (T)0);
+}
+
+}  // namespace tq

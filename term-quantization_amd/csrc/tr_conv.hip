@@ -1,0 +1,275 @@
+// Term-pair Conv2d on CDNA4 VALU (no MFMA) -- the accumulation the reference leaves to a
+// dense fp32 cuDNN conv of fake-quantized tensors (tr_layer.py:124-126).
+//
+// A TR'd activation is sf_x * v_x and a TR'd weight is sf_w * v_w with v_x, v_w the signed
+// sums of their kept HESE terms.  The term-pair sum of one output is
+//     sum_k sum_{tx in terms(x_k)} sum_{tw in terms(w_k)} tx * tw  ==  sum_k v_x[k] * v_w[k]
+// exactly (shift-adds of +-2^(ex+ew) are integer products of the term sums), so the kernel
+// accumulates integer products of int16 term sums with packed v_dot2c_i32_i16 (two term-sum
+// products per lane-op, exact int32 accumulation), and rounds once in the epilogue:
+//     y = fp32( double(acc) * (double(sf_x) * double(sf_w)) ) + bias.
+//
+// Data layout in HBM:
+//   activation codes  [N][H][W][Cp] int16 (NHWC, channels padded to Cp % 8 == 0 with 0)
+//   weight codes      [Cout_pad][Kp] int16, k = (kh*KW + kw)*Cp + c, Kp % 32 == 0, zero pad
+//   output            fp32, NCHW or NHWC (channels_last), bias optional
+//
+// Implicit GEMM: M = Cout, N = output pixels (N*Ho*Wo), K = KH*KW*Cp, K-step 32 (16 int16
+// pairs).  256 threads, each owns an 8 (Cout) x 8 (pixel) int32 accumulator tile; operands
+// are staged through LDS as [k-pair][m] / [k-pair][n] dwords (double-buffered, one barrier
+// per K-step) and read with ds_read_b128; the next K-step's global loads are issued before
+// the current step's 1024 dot2 per lane.
+#include "tq_device.h"
+#include "tq_launch.h"
+
+namespace tq {
+
+namespace {
+
+constexpr int kConvThreads = 256;
+
+__device__ __forceinline__ int dot2(int a, int b, int c) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, a), __builtin_bit_cast(s2, b), c, false);
+}
+
+template <int BM, int BN, bool OUT_NHWC>
+__global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) {
+  constexpr int TX = BN / 8;
+  static_assert((BM / 8) * TX == kConvThreads, "8x8 per thread");
+  constexpr int A_LOADS = BM * 4 / kConvThreads;  // 16-B vectors per thread per K-step
+  constexpr int B_LOADS = BN * 4 / kConvThreads;
+
+  __shared__ __attribute__((aligned(16))) int32_t As[2][16][BM];
+  __shared__ __attribute__((aligned(16))) int32_t Bs[2][16][BN];
+
+  const int tid = threadIdx.x;
+  const int tx = tid % TX;
+  const int ty = tid / TX;
+  const int m0 = blockIdx.y * BM;
+  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+
+  // Load-slot geometry: a 16-B vector = 8 int16 codes = 4 k-pairs.  Lanes 0-15 of a
+  // 16-lane quarter take 16 rows (pixels) at the same k-vector v, so one ds_write_b32
+  // instruction touches at most 2 lanes per bank.
+  const int v = (tid >> 4) & 3;
+  const int rowl = (tid & 15) + 16 * (tid >> 6);  // + 64*r for slot r
+
+  // Activation slots: per-pixel origin and row base.
+  int64_t pbase[B_LOADS];
+  int ih0[B_LOADS], iw0[B_LOADS];
+#pragma unroll
+  for (int r = 0; r < B_LOADS; ++r) {
+    const int64_t p = n0 + rowl + 64 * r;
+    if (p < a.P) {
+      const int64_t img = p / HoWo;
+      const int64_t rem = p - img * HoWo;
+      const int oh = (int)(rem / a.Wo);
+      const int ow = (int)(rem - (int64_t)oh * a.Wo);
+      ih0[r] = oh * a.sh - a.ph;
+      iw0[r] = ow * a.sw - a.pw;
+      pbase[r] = img * a.H;
+    } else {
+      ih0[r] = -(1 << 28);  // never in bounds
+      iw0[r] = 0;
+      pbase[r] = 0;
+    }
+  }
+  // k-vector state of this lane (shared by all its activation slots)
+  int kc = v * 8;  // channel within tap
+  int kr = 0, ks = 0, ktap = 0;
+  while (kc >= a.Cp) {
+    kc -= a.Cp;
+    ++ktap;
+    if (++ks == a.KW) {
+      ks = 0;
+      ++kr;
+    }
+  }
+
+  const int16_t* __restrict__ wrow[A_LOADS];
+#pragma unroll
+  for (int r = 0; r < A_LOADS; ++r)
+    wrow[r] = a.w + (int64_t)(m0 + rowl + 64 * r) * a.Kp + v * 8;
+
+  const int ntaps = a.KH * a.KW;
+  const int nsteps = a.Kp / 32;
+
+  int4 ra[A_LOADS], rb[B_LOADS];
+  auto load_tile = [&](int step) {
+#pragma unroll
+    for (int r = 0; r < A_LOADS; ++r)
+      ra[r] = *reinterpret_cast<const int4*>(wrow[r] + step * 32);
+#pragma unroll
+    for (int r = 0; r < B_LOADS; ++r) {
+      rb[r] = make_int4(0, 0, 0, 0);
+      if (ktap < ntaps) {
+        const int ih = ih0[r] + kr * a.dh;
+        const int iw = iw0[r] + ks * a.dw;
+        if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+          rb[r] = *reinterpret_cast<const int4*>(a.x + ((pbase[r] + ih) * a.W + iw) * a.Cp + kc);
+      }
+    }
+    // advance this lane's k-vector by 32 codes
+    kc += 32;
+    while (kc >= a.Cp) {
+      kc -= a.Cp;
+      ++ktap;
+      if (++ks == a.KW) {
+        ks = 0;
+        ++kr;
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < A_LOADS; ++r) {
+      const int m = rowl + 64 * r;
+      As[buf][v * 4 + 0][m] = ra[r].x;
+      As[buf][v * 4 + 1][m] = ra[r].y;
+      As[buf][v * 4 + 2][m] = ra[r].z;
+      As[buf][v * 4 + 3][m] = ra[r].w;
+    }
+#pragma unroll
+    for (int r = 0; r < B_LOADS; ++r) {
+      const int n = rowl + 64 * r;
+      Bs[buf][v * 4 + 0][n] = rb[r].x;
+      Bs[buf][v * 4 + 1][n] = rb[r].y;
+      Bs[buf][v * 4 + 2][n] = rb[r].z;
+      Bs[buf][v * 4 + 3][n] = rb[r].w;
+    }
+  };
+
+  int acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) load_tile(step + 1);
+#pragma unroll 2
+    for (int kk = 0; kk < 16; ++kk) {
+      const int4 a0 = *reinterpret_cast<const int4*>(&As[cur][kk][ty * 4]);
+      const int4 a1 = *reinterpret_cast<const int4*>(&As[cur][kk][BM / 2 + ty * 4]);
+      const int4 b0 = *reinterpret_cast<const int4*>(&Bs[cur][kk][tx * 4]);
+      const int4 b1 = *reinterpret_cast<const int4*>(&Bs[cur][kk][BN / 2 + tx * 4]);
+      const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const int bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = dot2(av[i], bv[j], acc[i][j]);
+    }
+    if (step + 1 < nsteps) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: one rounding of the exact integer sum, then bias (fp32, as conv + bias).
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int co = m0 + (i < 4 ? ty * 4 + i : BM / 2 + ty * 4 + (i - 4));
+    if (co >= a.Cout) continue;
+    const float b = a.bias ? a.bias[co] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
+      if (p >= a.P) continue;
+      const float y = (float)((double)acc[i][j] * a.scale) + b;
+      if (OUT_NHWC) {
+        a.out[p * a.Cout + co] = y;
+      } else {
+        const int64_t img = p / HoWo;
+        a.out[(img * a.Cout + co) * HoWo + (p - img * HoWo)] = y;
+      }
+    }
+  }
+}
+
+// TR of fp32 activations straight into int16 NHWC codes (group_size 1, the reference's
+// activation call, tr_layer.py:96-99).  One lane per 8 channels of one pixel.
+template <bool IN_NHWC>
+__global__ __launch_bounds__(256) void act_encode_kernel(const float* __restrict__ x,
+                                                         int16_t* __restrict__ codes,
+                                                         int64_t npix, int64_t HW, int C,
+                                                         int Cp, float sf, float maxv, int k) {
+  const int chunks = Cp / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= npix * chunks) return;
+  const int64_t pix = t / chunks;
+  const int c0 = (int)(t - pix * chunks) * 8;
+  int32_t v[8];
+  if (IN_NHWC && Cp == C) {
+    const float4 x0 = *reinterpret_cast<const float4*>(x + pix * C + c0);
+    const float4 x1 = *reinterpret_cast<const float4*>(x + pix * C + c0 + 4);
+    const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = tr_value_g1(xs[i], sf, maxv, k);
+  } else {
+    const int64_t img = pix / HW;
+    const int64_t s = pix - img * HW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      v[i] = 0;
+      if (c < C) {
+        const float xv = IN_NHWC ? x[pix * C + c] : x[(img * C + c) * HW + s];
+        v[i] = tr_value_g1(xv, sf, maxv, k);
+      }
+    }
+  }
+  int4 packed;
+  packed.x = (v[0] & 0xFFFF) | (v[1] << 16);
+  packed.y = (v[2] & 0xFFFF) | (v[3] << 16);
+  packed.z = (v[4] & 0xFFFF) | (v[5] << 16);
+  packed.w = (v[6] & 0xFFFF) | (v[7] << 16);
+  *reinterpret_cast<int4*>(codes + pix * Cp + c0) = packed;
+}
+
+}  // namespace
+
+hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
+                             int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,
+                             hipStream_t stream) {
+  const float maxv = (float)((1u << bitwidth) - 1u);
+  const int64_t npix = N * H * W;
+  const int64_t n = npix * (Cp / 8);
+  if (n == 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (in_nhwc)
+    act_encode_kernel<true><<<grid, 256, 0, stream>>>(x, codes, npix, H * W, (int)C, (int)Cp,
+                                                       sf, maxv, k);
+  else
+    act_encode_kernel<false><<<grid, 256, 0, stream>>>(x, codes, npix, H * W, (int)C, (int)Cp,
+                                                        sf, maxv, k);
+  return hipGetLastError();
+}
+
+int conv_tile_m(int64_t cout) { return cout <= 64 ? 64 : 128; }
+
+hipError_t launch_conv2d_tp(const ConvArgs& a, int out_nhwc, hipStream_t stream) {
+  if (a.P == 0 || a.Cout == 0) return hipSuccess;
+  const int bm = conv_tile_m(a.Cout);
+  if (bm == 64) {
+    const dim3 grid((unsigned)((a.P + 255) / 256), (unsigned)((a.Cout + 63) / 64));
+    if (out_nhwc)
+      conv2d_tp_kernel<64, 256, true><<<grid, kConvThreads, 0, stream>>>(a);
+    else
+      conv2d_tp_kernel<64, 256, false><<<grid, kConvThreads, 0, stream>>>(a);
+  } else {
+    const dim3 grid((unsigned)((a.P + 127) / 128), (unsigned)((a.Cout + 127) / 128));
+    if (out_nhwc)
+      conv2d_tp_kernel<128, 128, true><<<grid, kConvThreads, 0, stream>>>(a);
+    else
+      conv2d_tp_kernel<128, 128, false><<<grid, kConvThreads, 0, stream>>>(a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace tq

@@ -1,0 +1,142 @@
+"""ctypes binding of libtq_hip.so (include/tq.h) for torch tensors.
+
+This is the only place the Python host layer touches native code.  The library is built
+in-tree (``make -C term-quantization_amd`` or ``__graft_entry__.build()``) and loaded from
+``term-quantization_amd/lib/libtq_hip.so``; if it is missing every op raises -- there is no
+CPU or PyTorch fallback for the TQ path.
+
+Every call enqueues on torch's current HIP stream of the tensor's device, so the ops order
+correctly with surrounding torch work and can be captured into a CUDA/HIP graph.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtq_hip.so")
+
+_lib = None
+_lock = threading.Lock()
+
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+_vp = ctypes.c_void_p
+
+# name -> argtypes (all return int status unless listed in _RESTYPE)
+_SIGNATURES = {
+    "tq_version": [],
+    "tq_last_error": [],
+    "tq_tr_f32": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
+    "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
+    "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
+                         _vp],
+    "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _vp],
+    "tq_conv2d_cout_align": [],
+    "tq_conv2d_termpair": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64,
+                           _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32,
+                           _vp],
+    "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
+}
+_RESTYPE = {"tq_version": ctypes.c_char_p, "tq_last_error": ctypes.c_char_p,
+            "tq_conv2d_cout_align": _i64}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libtq_hip.so once; raise if it has not been built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise NativeLibraryMissing(
+                        "term-quantization HIP library not found at %s; build it with "
+                        "`make -C term-quantization_amd` (there is no CPU fallback)" % LIB_PATH)
+                l = ctypes.CDLL(LIB_PATH)
+                for name, argtypes in _SIGNATURES.items():
+                    fn = getattr(l, name)
+                    fn.argtypes = argtypes
+                    fn.restype = _RESTYPE.get(name, ctypes.c_int)
+                _lib = l
+    return _lib
+
+
+def version():
+    return lib().tq_version().decode()
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().tq_last_error().decode()
+        raise RuntimeError(msg)
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def tr_into(inp, out, sf, bitwidth, group_size, num_keep_terms, codes=None):
+    """Launch the TR op (tq_tr_f32 / tq_tr_f64 / tq_tr_encode_f32) on contiguous tensors."""
+    shape = (_i64 * inp.dim())(*inp.shape)
+    with torch.cuda.device(inp.device):
+        if codes is not None:
+            rc = lib().tq_tr_encode_f32(_ptr(inp), _ptr(out), _ptr(codes), inp.dim(), shape,
+                                        sf, bitwidth, group_size, num_keep_terms, _stream(inp))
+        elif inp.dtype == torch.float32:
+            rc = lib().tq_tr_f32(_ptr(inp), _ptr(out), inp.dim(), shape, sf, bitwidth,
+                                 group_size, num_keep_terms, _stream(inp))
+        else:
+            rc = lib().tq_tr_f64(_ptr(inp), _ptr(out), inp.dim(), shape, sf, bitwidth,
+                                 group_size, num_keep_terms, _stream(inp))
+    _check(rc)
+    return out
+
+
+def act_encode(x, in_nhwc, sf, bitwidth, num_keep_terms, codes):
+    n, c, h, w = x.shape
+    with torch.cuda.device(x.device):
+        rc = lib().tq_act_encode(_ptr(x), int(in_nhwc), n, c, h, w, sf, bitwidth,
+                                 num_keep_terms, _ptr(codes), codes.shape[-1], _stream(x))
+    _check(rc)
+    return codes
+
+
+def conv2d_cout_align():
+    return int(lib().tq_conv2d_cout_align())
+
+
+def conv2d_termpair(codes, w_codes, cout, kh, kw, stride, padding, dilation, scale, bias, out,
+                    out_nhwc):
+    n, h, w, cp = codes.shape
+    ho, wo = out.shape[2], out.shape[3]
+    with torch.cuda.device(codes.device):
+        rc = lib().tq_conv2d_termpair(_ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw,
+                                      w_codes.shape[1], stride[0], stride[1], padding[0],
+                                      padding[1], dilation[0], dilation[1], float(scale),
+                                      _ptr(bias), _ptr(out), ho, wo, int(out_nhwc),
+                                      _stream(codes))
+    _check(rc)
+    return out
+
+
+def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
+    """errs[s] (float64) for each candidate scale factor in sfs (tq_mse_profile)."""
+    errs = torch.empty(sfs.numel(), dtype=torch.float64, device=x.device)
+    with torch.cuda.device(x.device):
+        rc = lib().tq_mse_profile(_ptr(x), _ptr(hist), x.numel(), _ptr(sfs), sfs.numel(),
+                                  int(bitwidth), int(num_keep_terms), _ptr(errs), _stream(x))
+    _check(rc)
+    return errs

@@ -1,0 +1,145 @@
+"""Functional TQ ops on torch tensors, all backed by libtq_hip.so (tq_native).
+
+  tr(input, sf, bitwidth, group_size, num_keep_terms)     reference tr_cuda.tr, same contract
+  tr_elementwise(x, sf, bitwidth, num_keep_terms)          group_size-1 TR of any dense layout
+  tr_encode(w, sf, bitwidth, group_size, num_keep_terms)   TR(w) plus its integer term sums
+  pack_conv_weight(codes)                                  [O,I,KH,KW] int32 -> [O_pad, Kp] int16
+  tr_conv2d(x, ...)                                        conv2d(TR(x), TR(w)) by term pairs
+
+Errors mirror the reference boundary (kernels/tr_cuda.cpp:12-18): RuntimeError for a non-CUDA
+or non-contiguous input, a RuntimeError for an unsupported dtype, IndexError for < 2 dims.
+"""
+import torch
+
+import tq_native
+
+ACT_CHANNEL_ALIGN = 8   # int16 codes per 16-byte vector
+K_ALIGN = 32            # codes per K-step of the term-pair kernel
+MAX_CODE_BITS = 14      # |code| <= 2^bitwidth must fit int16
+
+
+def _check_input(input):
+    # kernels/tr_cuda.cpp:12-18 (CHECK_CUDA, CHECK_CONTIGUOUS) and the dispatch dtype check
+    if not isinstance(input, torch.Tensor):
+        raise TypeError("tr(): input must be a torch.Tensor")
+    if not input.is_cuda:
+        raise RuntimeError("input must be a CUDA tensor")
+    if not input.is_contiguous():
+        raise RuntimeError("input must be contiguous")
+    if input.dtype not in (torch.float32, torch.float64):
+        raise RuntimeError('"tr_cuda" not implemented for \'%s\'' % str(input.dtype).replace(
+            "torch.", "").capitalize())
+    if input.dim() < 2:
+        # input.size(1) on a 0-/1-D tensor (kernels/tr_cuda_kernel.cu:135)
+        raise IndexError("Dimension out of range (expected to be in range of [-%d, %d], but "
+                         "got 1)" % (max(input.dim(), 1), max(input.dim() - 1, 0)))
+
+
+def tr(input, sf, bitwidth, group_size, num_keep_terms):
+    """Term-revealing op: ``tr_cuda.tr`` of the reference (kernels/tr_cuda.cpp:20-28).
+
+    Returns a new tensor of the input's shape and dtype holding sf * (sum of the kept HESE
+    terms) per element; ``sf`` is narrowed to float32 as at the pybind boundary."""
+    _check_input(input)
+    out = torch.empty_like(input, memory_format=torch.contiguous_format)
+    if input.numel() == 0:
+        return out
+    return tq_native.tr_into(input, out, float(sf), int(bitwidth), int(group_size),
+                             int(num_keep_terms))
+
+
+def tr_elementwise(x, sf, bitwidth, num_keep_terms):
+    """group_size-1 TR (the activation call, tr_layer.py:96-99) on any dense tensor.
+
+    Elementwise, so a channels_last (or otherwise permuted but dense) tensor is processed in
+    its own memory order and the result keeps the input's strides."""
+    if not x.is_cuda:
+        raise RuntimeError("input must be a CUDA tensor")
+    if x.dtype not in (torch.float32, torch.float64):
+        raise RuntimeError('"tr_cuda" not implemented for \'%s\'' % str(x.dtype))
+    if x.is_contiguous():
+        flat = x.view(1, -1, 1, 1)
+        return tr(flat, sf, bitwidth, 1, num_keep_terms).view(x.shape)
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        base = x.permute(0, 2, 3, 1)  # contiguous NHWC view of the same storage
+        out = tr(base.reshape(1, -1, 1, 1), sf, bitwidth, 1, num_keep_terms)
+        return out.view(base.shape).permute(0, 3, 1, 2)
+    return tr(x.contiguous().view(1, -1, 1, 1), sf, bitwidth, 1,
+              num_keep_terms).view(x.shape)
+
+
+def tr_encode(w, sf, bitwidth, group_size, num_keep_terms):
+    """(TR(w), v) with TR(w) == v * fp32(sf) exactly; v int32 with w's shape."""
+    _check_input(w)
+    if w.dtype != torch.float32:
+        raise RuntimeError("tr_encode: float32 only")
+    out = torch.empty_like(w)
+    codes = torch.empty(w.shape, dtype=torch.int32, device=w.device)
+    if w.numel() == 0:
+        return out, codes
+    tq_native.tr_into(w, out, float(sf), int(bitwidth), int(group_size), int(num_keep_terms),
+                      codes=codes)
+    return out, codes
+
+
+def round_up(v, m):
+    return (v + m - 1) // m * m
+
+
+def act_channels(c):
+    return round_up(c, ACT_CHANNEL_ALIGN)
+
+
+def pack_conv_weight(codes):
+    """[O, I, KH, KW] int32 term sums -> int16 [O_pad, Kp] with k = (kh*KW + kw)*Cp + c.
+
+    Layout plumbing done once per layer at construction; returns (packed, Cp)."""
+    o, i, kh, kw = codes.shape
+    cp = act_channels(i)
+    t = codes.permute(0, 2, 3, 1)  # O, KH, KW, I
+    if cp != i:
+        t = torch.nn.functional.pad(t, (0, cp - i))
+    t = t.reshape(o, kh * kw * cp)
+    kp = round_up(kh * kw * cp, K_ALIGN)
+    o_pad = round_up(o, tq_native.conv2d_cout_align())
+    packed = torch.zeros((o_pad, kp), dtype=torch.int16, device=codes.device)
+    packed[:o, :kh * kw * cp] = t.to(torch.int16)
+    return packed.contiguous(), cp
+
+
+def conv_out_size(h, k, s, p, d):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_channels,
+              kernel_size, stride, padding, dilation):
+    """conv2d(TR(x), TR(w)) + bias by exact term-pair accumulation (groups = 1).
+
+    x: fp32 [N, C, H, W] CUDA tensor, NCHW-contiguous or channels_last.  The output has the
+    conv's shape and the input's memory format (as cuDNN/MIOpen convs do)."""
+    if not x.is_cuda:
+        raise RuntimeError("input must be a CUDA tensor")
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("tr_conv2d: expects a 4-D float32 input")
+    n, c, h, w = x.shape
+    if act_channels(c) != cp:
+        raise RuntimeError("tr_conv2d: input has %d channels, weights expect %d" % (c, cp))
+    nhwc = (not x.is_contiguous()) and x.is_contiguous(memory_format=torch.channels_last)
+    if not nhwc and not x.is_contiguous():
+        x = x.contiguous()
+    kh, kw = kernel_size
+    ho = conv_out_size(h, kh, stride[0], padding[0], dilation[0])
+    wo = conv_out_size(w, kw, stride[1], padding[1], dilation[1])
+    codes = torch.empty((n, h, w, cp), dtype=torch.int16, device=x.device)
+    tq_native.act_encode(x, nhwc, float(sf_x), int(data_bits), int(data_terms), codes)
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    out = torch.empty((n, out_channels, ho, wo), dtype=torch.float32, device=x.device,
+                      memory_format=fmt)
+    # one rounding of the exact integer sum: scale = fp32(sf_x) * fp32(sf_w) in double
+    scale = float(torch.tensor(sf_x, dtype=torch.float32)) * float(
+        torch.tensor(sf_w, dtype=torch.float32))
+    if bias is not None:
+        bias = bias.detach().to(torch.float32).contiguous()
+    tq_native.conv2d_termpair(codes, w_packed, out_channels, kh, kw, stride, padding, dilation,
+                              scale, bias, out, nhwc)
+    return out

@@ -1,0 +1,290 @@
+"""Term-quantization module API -- the drop-in for the reference's tr_layer.py.
+
+Same public names, constructor signatures, attributes and behaviour as the reference
+(tr_layer.py:1-201): ``tr_cuda`` (an object with ``.tr``), ``hese``, ``mse_profile``,
+``compute_compressed_hese``, ``set_tr_tracking``, ``LinearQuantize``, ``TRConv2dLayer``,
+``TRLinearLayer`` and ``TRLSTMLayer``.  Underneath, every TR runs in the MI355X HIP library
+(libtq_hip.so), and a converted Conv2d no longer runs a dense fp32 conv of fake-quantized
+tensors: it accumulates term pairs exactly in the term-pair kernel (tq_ops.tr_conv2d).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+import tq_native
+import tq_ops
+
+
+class _TRExtension(object):
+    """Stands where ``tr_cuda = load('tr_cuda', [...])`` stood (tr_layer.py:7): a module-like
+    object whose ``tr`` is the reference pybind entry (kernels/tr_cuda.cpp:20-28)."""
+
+    __name__ = "tr_cuda"
+
+    @staticmethod
+    def tr(input, sf, bitwidth, group_size, num_keep_terms):
+        return tq_ops.tr(input, sf, bitwidth, group_size, num_keep_terms)
+
+
+tr_cuda = _TRExtension()
+
+
+def hese(number):
+    """tr_layer.hese (tr_layer.py:9-41): the run-based HESE variant used for parameter-bit
+    counting.  Each run of ones from bit a up to bit b becomes (-2^a, +2^(b+1)), and a run of
+    length one collapses to the single term +2^a ("merging neighbors hack").  Terms come out
+    least significant run first, signed by the number's sign."""
+    sign = -1 if number < 0 else 1
+    q = abs(int(number))
+    terms = []
+    i = 0
+    while q >> i:
+        if (q >> i) & 1:
+            j = i
+            while (q >> j) & 1:
+                j += 1
+            if j == i + 1:
+                terms.append(sign * (1 << i))
+            else:
+                terms.append(-sign * (1 << i))
+                terms.append(sign * (1 << j))
+            i = j
+        else:
+            i += 1
+    return terms
+
+
+def _hese_len_tensor(q):
+    """len(hese(q)) for every element of an integer tensor: 2 terms per run of ones, 1 for
+    a run of length one."""
+    q = q.abs().to(torch.int64)
+    starts = q & ~(q << 1)
+    singles = starts & ~(q >> 1)
+
+    def popcount(v):
+        c = torch.zeros_like(v)
+        while bool((v != 0).any()):
+            c += v & 1
+            v = v >> 1
+        return c
+
+    return 2 * popcount(starts) - popcount(singles)
+
+
+def mse_profile(hist, minv, maxv, bit_width, terms):
+    """Activation scale factor by weighted-MSE search (tr_layer.py:43-54).
+
+    Same candidate grid (2048 fp32 sfs in linspace(1e-8, maxv)) and the same histogram grid
+    as the reference; all 2048 candidates are scored in one HIP launch (tq_mse_profile) and
+    the first arg-min is returned as a Python float, like ``sfs[min_idx]``."""
+    device = hist.device if hist.is_cuda else torch.device("cuda")
+    x = torch.linspace(minv, maxv, len(hist)).to(device)
+    sfs_list = torch.linspace(1e-8, maxv, 2048).tolist()
+    sfs = torch.tensor(sfs_list, dtype=torch.float32, device=device)
+    h = hist.detach().to(device=device, dtype=torch.float32).contiguous()
+    errs = tq_native.mse_profile(x.contiguous(), h, sfs, bit_width, terms)
+    min_idx = int(torch.argmin(errs).item())
+    return sfs_list[min_idx]
+
+
+def compute_compressed_hese(w, sf, weight_terms):
+    """Parameter bits of HESE-compressed weights (tr_layer.py:57-63).  The reference loops
+    over every weight in Python; this counts the same terms with tensor ops."""
+    exp_bits = math.ceil(math.log2(weight_terms))
+    bit_width = exp_bits + 2  # 1 for sign, 1 for barrier
+    w = (w / sf).int()
+    return int(bit_width * int(_hese_len_tensor(w).sum().item()))
+
+
+def set_tr_tracking(model, tracking):
+    """Switch every TR layer between calibration and quantized mode (tr_layer.py:66-76)."""
+    for name, layer in model.named_modules():
+        if isinstance(layer, (TRLinearLayer, TRLSTMLayer, TRConv2dLayer)):
+            module_keys = name.split('.')
+            module = model
+            for k in module_keys[:-1]:
+                module = module._modules[k]
+
+            module._modules[module_keys[-1]].tracking(tracking)
+
+    return model
+
+
+class LinearQuantize(nn.Module):
+    """Per-layer activation quantizer (tr_layer.py:78-104).
+
+    While ``tracking``: accumulates an 8192-bin histogram over [-50, 50] and returns x.
+    Afterwards: TR with group size 1, ``data_bits`` bits and ``data_terms`` kept terms."""
+
+    def __init__(self, data_bits, data_terms):
+        super(LinearQuantize, self).__init__()
+        self.sf = 1
+        self.num_bins = 8192
+        self.minv = -50
+        self.maxv = 50
+        self.register_buffer('hist_bins', torch.Tensor(self.num_bins).zero_())
+        self.tracking = True
+        self.data_bits = data_bits
+        self.data_terms = data_terms
+
+    def forward(self, x):
+        if self.tracking:
+            self.hist_bins += torch.histc(x, self.num_bins, self.minv, self.maxv)
+            return x
+
+        return tq_ops.tr_elementwise(x, self.sf, self.data_bits, self.data_terms)
+
+    def finish_tracking(self):
+        self.sf = mse_profile(self.hist_bins, self.minv, self.maxv,
+                              self.data_bits, self.data_terms)
+        self.tracking = False
+
+
+def _w_sf(w, weight_bits):
+    max_wq = 2**(weight_bits - 1)
+    return w.abs().max().item() / max_wq
+
+
+class TRConv2dLayer(nn.Module):
+    """Conv2d with term-revealed weights and activations (tr_layer.py:106-132).
+
+    Construction TRs the weight with group size ``group_size`` and budget ``num_terms`` and
+    keeps the fake-quantized tensor as ``self.conv.weight`` (so ``profile_model`` and any
+    caller reading the weight see the reference values).  It also keeps the integer term
+    sums, packed for the term-pair kernel, in the ``w_codes`` buffer.
+
+    forward: while tracking, ``self.conv`` on the unquantized input (the reference returns x
+    from the quantizer while tracking); afterwards ``tr_conv2d`` -- conv2d(TR(x), TR(w)) + bias
+    by exact term-pair accumulation -- when the layer fits the term-pair kernel (groups 1,
+    data/weight bits <= 14, zero padding), else the reference's own composition
+    ``self.conv(self.input_quant(x))`` with the HIP TR op (``self.termpair`` says which)."""
+
+    def __init__(self, conv_layer, data_bits=8, data_terms=4, weight_bits=8,
+                 group_size=1, num_terms=8):
+        super(TRConv2dLayer, self).__init__()
+        device = conv_layer.weight.device
+        self.data_bits = data_bits
+        self.data_terms = data_terms
+        self.input_quant = LinearQuantize(data_bits, data_terms).to(device)
+        self.group_size = group_size
+        self.num_terms = num_terms
+        self.weight_bits = weight_bits
+        w = conv_layer.weight
+        self.w_sf = _w_sf(w, weight_bits)
+        self.termpair = (conv_layer.groups == 1 and weight_bits <= tq_ops.MAX_CODE_BITS
+                         and data_bits <= tq_ops.MAX_CODE_BITS
+                         and getattr(conv_layer, 'padding_mode', 'zeros') == 'zeros'
+                         and not isinstance(conv_layer.padding, str)
+                         and w.dtype == torch.float32)
+        if self.termpair:
+            wq, codes = tq_ops.tr_encode(w.detach().contiguous(), self.w_sf, weight_bits,
+                                         group_size, num_terms)
+            packed, cp = tq_ops.pack_conv_weight(codes)
+            # int32 accumulator bound: sum_k |v_w| * max|v_x| (|v_x| <= 2^data_bits)
+            bound = codes.abs().to(torch.int64).flatten(1).sum(1).max().item() << data_bits
+            self.termpair = bound < 2**31
+        else:
+            wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
+        if self.termpair:
+            self.register_buffer('w_codes', packed)
+            self.act_channels = cp
+        else:
+            self.register_buffer('w_codes', None)
+        conv_layer.weight = nn.Parameter(wq)
+        self.conv = conv_layer
+
+    def forward(self, x):
+        if self.input_quant.tracking or not self.termpair:
+            xq = self.input_quant(x)
+            return self.conv(xq)
+        c = self.conv
+        return tq_ops.tr_conv2d(x, self.input_quant.sf, self.data_bits, self.data_terms,
+                                self.w_codes, self.act_channels, self.w_sf, c.bias,
+                                c.out_channels, c.kernel_size, c.stride, c.padding, c.dilation)
+
+    def tracking(self, tracking):
+        if not tracking:
+            self.input_quant.finish_tracking()
+        else:
+            self.input_quant.tracking = True
+
+
+class TRLinearLayer(nn.Module):
+    """Linear with term-revealed weights (tr_layer.py:134-160).
+
+    Like the reference, forward returns ``self.linear(x)`` on the UNquantized input
+    (tr_layer.py:152-154): only the weights are term-quantized.  The input quantizer still
+    records its histogram while tracking; after calibration the reference computes TR(x) and
+    discards it, which this layer skips (the output is identical)."""
+
+    def __init__(self, linear_layer, data_bits=8, data_terms=4, weight_bits=8,
+                 group_size=1, num_terms=8):
+        super(TRLinearLayer, self).__init__()
+        device = linear_layer.weight.device
+        self.data_bits = data_bits
+        self.data_terms = data_terms
+        self.input_quant = LinearQuantize(data_bits, data_terms).to(device)
+        self.group_size = group_size
+        self.num_terms = num_terms
+        self.weight_bits = weight_bits
+        w = linear_layer.weight
+        self.w_sf = _w_sf(w, weight_bits)
+        w = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
+        linear_layer.weight = nn.Parameter(w)
+        self.linear = linear_layer
+
+    def forward(self, x):
+        if self.input_quant.tracking:
+            self.input_quant(x)
+        return self.linear(x)
+
+    def tracking(self, tracking):
+        if not tracking:
+            self.input_quant.finish_tracking()
+        else:
+            self.input_quant.tracking = True
+
+
+class TRLSTMLayer(nn.Module):
+    """LSTM with term-revealed layer-0 weights and quantized inputs/hidden state
+    (tr_layer.py:162-201); ``w_sf`` ends up as the weight_hh_l0 scale, as in the reference."""
+
+    def __init__(self, lstm_layer, data_bits=8, data_terms=4, weight_bits=8,
+                 group_size=1, num_terms=8):
+        super(TRLSTMLayer, self).__init__()
+        device = lstm_layer.weight_ih_l0.device
+        self.data_bits = data_bits
+        self.data_terms = data_terms
+        self.input_quant = LinearQuantize(data_bits, data_terms).to(device)
+        self.group_size = group_size
+        self.num_terms = num_terms
+        self.weight_bits = weight_bits
+
+        # ih_l0
+        w = lstm_layer.weight_ih_l0
+        self.w_sf = _w_sf(w, weight_bits)
+        wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
+        lstm_layer.weight_ih_l0 = nn.Parameter(wq)
+
+        # hh_l0
+        w = lstm_layer.weight_hh_l0
+        self.w_sf = _w_sf(w, weight_bits)
+        wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
+        lstm_layer.weight_hh_l0 = nn.Parameter(wq)
+
+        self.lstm = lstm_layer
+        self.lstm.flatten_parameters()
+
+    def forward(self, emb, hidden):
+        embq = self.input_quant(emb)
+        hidden_qs = tuple(self.input_quant(h) for h in hidden)
+
+        return self.lstm(embq, hidden_qs)
+
+    def tracking(self, tracking):
+        if not tracking:
+            self.input_quant.finish_tracking()
+        else:
+            self.input_quant.tracking = True

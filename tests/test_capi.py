@@ -1,0 +1,89 @@
+"""The C-ABI library (include/tq.h) builds, loads and validates arguments -- CPU-only.
+
+No kernel is launched here (there is no GPU in the build container); every call below is
+rejected by argument validation before any HIP runtime call."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import tq_native
+import tq_ops
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "tq.h")).read()
+    return sorted(set(re.findall(r"\b(tq_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = tq_native.lib()
+    declared = _declared_symbols()
+    assert declared, "no declarations parsed from include/tq.h"
+    for name in declared:
+        assert hasattr(lib, name), name
+    # the Python binding covers exactly the header
+    assert sorted(tq_native.EXPORTED_SYMBOLS) == declared
+
+
+def test_library_is_gfx950_code_object():
+    data = open(tq_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version_and_error_channel():
+    assert tq_native.version().startswith("tq-hip")
+    lib = tq_native.lib()
+    shape = (ctypes.c_int64 * 1)(4)
+    rc = lib.tq_tr_f32(None, None, 1, shape, 1.0, 8, 1, 1, None)
+    assert rc == 1
+    assert b"at least 2 dimensions" in lib.tq_last_error()
+
+
+@pytest.mark.parametrize("args,code,msg", [
+    (dict(bw=25), 2, b"bitwidth"),
+    (dict(bw=-1), 2, b"bitwidth"),
+    (dict(g=0), 1, b"group_size"),
+    (dict(g=33), 1, b"group_size"),
+    (dict(sf=-1.0), 1, b"sf"),
+    (dict(sf=float("nan")), 1, b"sf"),
+])
+def test_tr_argument_validation(args, code, msg):
+    lib = tq_native.lib()
+    shape = (ctypes.c_int64 * 2)(4, 8)
+    p = dict(bw=8, g=1, sf=1.0)
+    p.update(args)
+    rc = lib.tq_tr_f32(None, None, 2, shape, p["sf"], p["bw"], p["g"], 1, None)
+    assert rc == code
+    assert msg in lib.tq_last_error()
+
+
+def test_conv_argument_validation():
+    lib = tq_native.lib()
+    rc = lib.tq_conv2d_termpair(None, 1, 8, 8, 12, None, 4, 3, 3, 128, 1, 1, 1, 1, 1, 1, 1.0,
+                                None, None, 8, 8, 0, None)
+    assert rc == 1 and b"cp" in lib.tq_last_error()
+    rc = lib.tq_conv2d_termpair(None, 1, 8, 8, 16, None, 4, 3, 3, 100, 1, 1, 1, 1, 1, 1, 1.0,
+                                None, None, 8, 8, 0, None)
+    assert rc == 1 and b"kp" in lib.tq_last_error()
+    rc = lib.tq_conv2d_termpair(None, 1, 8, 8, 16, None, 4, 3, 3, 160, 1, 1, 1, 1, 1, 1, 1.0,
+                                None, None, 7, 8, 0, None)
+    assert rc == 1 and b"output size" in lib.tq_last_error()
+    assert tq_native.conv2d_cout_align() == 128
+
+
+def test_act_encode_rejects_wide_codes():
+    lib = tq_native.lib()
+    rc = lib.tq_act_encode(None, 1, 1, 8, 2, 2, 1.0, 16, 3, None, 8, None)
+    assert rc == 2 and b"bitwidth" in lib.tq_last_error()
+
+
+def test_ops_reject_cpu_tensors_like_the_reference():
+    with pytest.raises(RuntimeError, match="CUDA"):
+        tq_ops.tr(torch.zeros(2, 4), 1.0, 8, 1, 1)
+    with pytest.raises(RuntimeError, match="CUDA"):
+        tq_ops.tr_elementwise(torch.zeros(2, 4), 1.0, 8, 1)

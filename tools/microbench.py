@@ -1,0 +1,94 @@
+"""Kernel microbenchmarks on one GPU: the TR op (D1) and each ResNet-18 TR conv at batch 256.
+
+    python tools/microbench.py [--batch 256] [--iters 20]
+
+Prints one line per kernel: average time (HIP events on the launch stream), achieved
+algorithmic GB/s (TR op, 8 B/elem; act encode, 6 B/elem) or term-sum MAC/s (conv)."""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
+
+import tq_native  # noqa: E402
+import tq_ops  # noqa: E402
+import tr_layer  # noqa: E402
+
+# (cin, cout, k, stride, hin) of the 19 ResNet-18 TR convs
+RESNET18_TR = [(64, 64, 3, 1, 56)] * 4 + [(64, 128, 3, 2, 56), (128, 128, 3, 1, 28),
+                                          (64, 128, 1, 2, 56)] + \
+    [(128, 128, 3, 1, 28)] * 2 + [(128, 256, 3, 2, 28), (256, 256, 3, 1, 14),
+                                  (128, 256, 1, 2, 28)] + \
+    [(256, 256, 3, 1, 14)] * 2 + [(256, 512, 3, 2, 14), (512, 512, 3, 1, 7),
+                                  (256, 512, 1, 2, 14)] + [(512, 512, 3, 1, 7)] * 2
+
+
+def time_fn(fn, iters, warmup=3):
+    for _ in range(warmup):
+        fn()
+    s = torch.cuda.current_stream()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record(s)
+    for _ in range(iters):
+        fn()
+    end.record(s)
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+
+    x = torch.relu(torch.randn(256, 64, 56, 56, device=dev))
+    flat = x.view(1, -1, 1, 1)
+    out = torch.empty_like(flat)
+    t = time_fn(lambda: tq_native.tr_into(flat, out, 0.05, 9, 1, 3), args.iters)
+    n = flat.numel()
+    print("tr_op D1 g=1: %.1f us  %.0f GB/s (8 B/elem)  %.3f Telem/s" % (
+        t * 1e6, 8 * n / t / 1e9, n / t / 1e12))
+
+    xl = x.to(memory_format=torch.channels_last)
+    codes = torch.empty((256, 56, 56, 64), dtype=torch.int16, device=dev)
+    t = time_fn(lambda: tq_native.act_encode(xl, True, 0.05, 9, 3, codes), args.iters)
+    print("act_encode NHWC: %.1f us  %.0f GB/s (6 B/elem)" % (t * 1e6, 6 * n / t / 1e9))
+
+    w = torch.randn(512, 512, 3, 3, device=dev) * 0.05
+    t = time_fn(lambda: tr_layer.tr_cuda.tr(w, w.abs().max().item() / 256, 9, 8, 12), 5)
+    print("tr_op weight 512x512x3x3 g=8 k=12: %.1f us" % (t * 1e6))
+
+    total_mac, total_t = 0, 0.0
+    for i, (cin, cout, k, s, hin) in enumerate(RESNET18_TR):
+        conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(dev)
+        layer = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+        layer.input_quant.tracking = False
+        layer.input_quant.sf = 0.02
+        xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
+            memory_format=torch.channels_last)
+        ho = (hin + 2 * (k // 2) - k) // s + 1
+        cp = tq_ops.act_channels(cin)
+        codes = torch.empty((args.batch, hin, hin, cp), dtype=torch.int16, device=dev)
+        tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
+        o = torch.empty((args.batch, cout, ho, ho), device=dev,
+                        memory_format=torch.channels_last)
+        fn = lambda: tq_native.conv2d_termpair(codes, layer.w_codes, cout, k, k, (s, s),
+                                               (k // 2, k // 2), (1, 1), 1e-4, None, o, True)
+        t = time_fn(fn, args.iters)
+        mac = args.batch * cout * ho * ho * cin * k * k
+        total_mac += mac
+        total_t += t
+        print("conv%02d %3d->%3d k%d s%d %2dx%2d: %8.1f us  %6.1f TMAC/s" % (
+            i + 1, cin, cout, k, s, hin, hin, t * 1e6, mac / t / 1e12))
+    print("conv total: %.2f ms  %.1f TMAC/s  -> %.0f img/s (convs only)" % (
+        total_t * 1e3, total_mac / total_t / 1e12, args.batch / total_t))
+
+
+if __name__ == "__main__":
+    main()
