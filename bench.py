@@ -1,0 +1,271 @@
+"""ResNet-18 TQ (g=8, alpha=k=12, wb=db=9, dt=3) inference throughput on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one TQ forward of one synthetic 256x3x224x224 batch per GPU (BASELINE.json
+configs[1]): the 19 converted convs run the term-pair kernel on HIP-encoded
+activations, everything else (stem conv, BN, ReLU, pooling, fc) is torch on the same
+stream.  Inputs are resident in HBM before timing.  Ranks run independent batches (weak
+scaling, no data-path collective); one all-reduce of the accuracy counters closes the
+timed region.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
+
+import cnn_models  # noqa: E402
+import profile_model  # noqa: E402
+import tq_ops  # noqa: E402
+import tr_layer  # noqa: E402
+import util  # noqa: E402
+
+METRIC = "term-pair MACs/sec + images/sec, ResNet-18 TQ g=8 at 1/2/4/8 MI355X"
+WB, G, K, DB, DT = 9, 8, 12, 9, 3
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes x clock = 78.6e12 lane-op/s
+# v_dot2c_i32_i16 issues at half the VALU rate on gfx950 (4 cycles per wave64; measured
+# 35.8e12 lane-op/s by tools/valu_peak.hip) and does 2 int16 MACs per lane-op:
+DOT2_PEAK = 2 * VALU_LANE_OPS / 2   # 78.6e12 term-sum MAC/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--cpu-sample", type=int, default=24,
+                    help="images in the CPU-baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+class KernelTimer(object):
+    """HIP events around the TQ kernels inside the timed region (tq_ops hook)."""
+
+    def __init__(self):
+        self.events = {}
+        self.work = {}
+
+    def __call__(self, name, work, fn):
+        s = torch.cuda.current_stream()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        r = fn()
+        b.record(s)
+        self.events.setdefault(name, []).append((a, b))
+        self.work[name] = self.work.get(name, 0) + work
+        return r
+
+    def summary(self):
+        out = {}
+        for name, evs in self.events.items():
+            t = sum(a.elapsed_time(b) for a, b in evs) * 1e-3
+            out[name] = {"launches": len(evs), "seconds": t, "work": self.work[name]}
+        return out
+
+
+def build_model(dev, batch, seed):
+    torch.manual_seed(0)
+    model = cnn_models.resnet18(pretrained=False).to(dev).eval()
+    settings = cnn_models.static_conv_layer_settings(model, WB, G, K)
+    qmodel = cnn_models.convert_model(model, settings, DB, DT)
+    qmodel = qmodel.to(memory_format=torch.channels_last)
+    assert all(m.termpair for m in qmodel.modules() if isinstance(m, tr_layer.TRConv2dLayer))
+    # term-pair MACs per image (profile_model, 1x3x224x224 -- evaluate_cnn.py:28-29)
+    tmacs, _ = profile_model.get_model_ops(qmodel, (torch.randn(1, 3, 224, 224, device=dev),))
+    # calibration: one tracking pass on this rank's calibration batch, histograms summed
+    # over ranks, then every rank runs the same mse_profile
+    calib = util.SyntheticImageNet(batch, batch, seed=1000 + seed, device=dev).batch(0)[0]
+    with torch.no_grad():
+        qmodel(calib.to(memory_format=torch.channels_last))
+    util.allreduce_histograms(qmodel)
+    tr_layer.set_tr_tracking(qmodel, False)
+    return model, qmodel, tmacs
+
+
+def cpu_baseline(model_fp, qmodel, nimg):
+    """The oracle (C restatement of the reference kernel, 1 thread) TR-ing every activation,
+    with the reference's dense fp32 torch conv (1 thread) on the fake-quantized tensors --
+    the reference algorithm on the host, timed on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import copy
+    import torch.nn as nn
+
+    class OracleTRConv(nn.Module):
+        def __init__(self, layer):
+            super(OracleTRConv, self).__init__()
+            self.conv = copy.deepcopy(layer.conv).cpu().float()
+            self.sf = layer.input_quant.sf
+            self.db, self.dt = layer.data_bits, layer.data_terms
+
+        def forward(self, x):
+            xq = oracle.tr(x.contiguous().numpy().reshape(1, -1, 1, 1), self.sf, self.db, 1,
+                           self.dt)
+            return self.conv(torch.from_numpy(xq).view(x.shape))
+
+    cpu = copy.deepcopy(model_fp).cpu().float().eval()
+    qmods = dict(qmodel.named_modules())
+    for name, m in list(cpu.named_modules()):
+        if name in qmods and isinstance(qmods[name], tr_layer.TRConv2dLayer):
+            parent = cpu
+            keys = name.split(".")
+            for k in keys[:-1]:
+                parent = parent._modules[k]
+            parent._modules[keys[-1]] = OracleTRConv(qmods[name])
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        x = util.SyntheticImageNet(nimg, nimg, seed=7).batch(0)[0]
+        with torch.no_grad():
+            cpu(x[:1])  # warm the allocator
+            t0 = time.perf_counter()
+            cpu(x)
+            dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(nthreads)
+    return {"value": nimg / dt, "unit": "images/s", "cores": 1, "kind": "port",
+            "sample": "%d synthetic 3x224x224 images, ResNet-18 TQ forward: oracle TR "
+                      "(oracle/tr_oracle.c, 1 thread) on every TR-layer activation + torch-CPU "
+                      "fp32 conv (1 thread) on the fake-quantized tensors; weight TR excluded "
+                      "(one-time conversion)" % nimg}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    model_fp, qmodel, tmacs_per_img = build_model(dev, args.batch, rank)
+
+    # resident synthetic inputs (two batches, alternated) and labels
+    data = util.SyntheticImageNet(2 * args.batch, args.batch, seed=rank, device=dev)
+    batches = []
+    for i in range(2):
+        x, y = data.batch(i)
+        batches.append((x.to(memory_format=torch.channels_last).contiguous(
+            memory_format=torch.channels_last), y))
+    counters = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    def step(i):
+        x, y = batches[i % 2]
+        out = qmodel(x)
+        counters[0] += (out.argmax(1) == y).sum()
+        counters[1] += y.numel()
+
+    with torch.no_grad():
+        for i in range(args.warmup):
+            step(i)
+        timer = KernelTimer()
+        tq_ops.set_kernel_hook(timer)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        if world > 1:
+            dist.all_reduce(counters)  # the one collective: accuracy counters
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        tq_ops.set_kernel_hook(None)
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    images = args.batch * args.steps * world
+    ips = images / elapsed
+    kt = timer.summary()
+
+    result = None
+    if rank == 0:
+        conv = kt["conv2d_termpair"]
+        enc = kt["act_encode"]
+        conv_t = conv["seconds"] / conv["launches"]
+        conv_work = conv["work"] / conv["launches"]
+        enc_t = enc["seconds"] / enc["launches"]
+        enc_bytes = enc["work"] / enc["launches"]
+        traffic = enc_traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            pmc = json.load(open(pmc_path))
+            traffic = pmc.get("conv2d_tp_bytes_per_launch")
+            enc_traffic = pmc.get("act_encode_bytes_per_launch")
+        result = {
+            "metric": METRIC,
+            "value": ips,
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16",
+            "data": "synthetic",
+            "config": {"workload": "resnet18-tq-g8-k12 (wb=db=9, dt=3), synthetic N(0,1) "
+                                   "3x224x224, random-init weights",
+                       "per_gpu_batch": args.batch, "global_batch": args.batch * world,
+                       "parallelism": "dp%d (batch-sharded, no data-path collective)" % world},
+            "term_pair_macs_per_image": tmacs_per_img,
+            "term_pair_macs_per_s": tmacs_per_img * ips,
+            "roofline": {
+                "kernel": "conv2d_tp_kernel (term-pair conv, int16 term sums, v_dot2c_i32_i16)",
+                "bound": "valu",
+                "achieved": conv_work / conv_t / 1e12,
+                "peak": DOT2_PEAK / 1e12,
+                "unit": "TMAC/s (int16 term-sum products)",
+                "frac": conv_work / conv_t / DOT2_PEAK,
+                "traffic": traffic,
+                "algorithmic_macs_per_launch": conv_work,
+                "avg_launch_us": conv_t * 1e6,
+                "launches": conv["launches"],
+                "share_of_step": conv["seconds"] / elapsed,
+            },
+            "roofline_tr": {
+                "kernel": "act_encode_kernel (TR of activations -> int16 codes)",
+                "bound": "hbm",
+                "achieved": enc_bytes / enc_t / 1e9,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": enc_bytes / enc_t / 1e9 / HBM_PEAK_GBS,
+                "traffic": enc_traffic,
+                "algorithmic_bytes_per_launch": enc_bytes,
+                "avg_launch_us": enc_t * 1e6,
+                "launches": enc["launches"],
+            },
+            "accuracy_counters": [int(v) for v in counters.tolist()],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(model_fp, qmodel, args.cpu_sample)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if result is not None:
+        print(json.dumps(result))
+
+
+if __name__ == "__main__":
+    main()

@@ -46,8 +46,17 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
   const int tid = threadIdx.x;
   const int tx = tid % TX;
   const int ty = tid / TX;
-  const int m0 = blockIdx.y * BM;
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  // XCD-aware tile order: blocks are dealt round-robin to the 8 XCDs (bid % 8), so give
+  // each XCD a contiguous run of logical tiles, Cout tiles of one pixel tile adjacent --
+  // neighbouring pixel tiles share halo rows and all Cout tiles share the activation tile,
+  // and both then hit the same XCD's L2.  Bijective for any grid size.
+  const int nblk = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int m0 = (tile % mt) * BM;
+  const int64_t n0 = (int64_t)(tile / mt) * BN;
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
 
   // Load-slot geometry: a 16-B vector = 8 int16 codes = 4 k-pairs.  Lanes 0-15 of a
@@ -172,21 +181,59 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
   }
 
   // Epilogue: one rounding of the exact integer sum, then bias (fp32, as conv + bias).
+  // 16-byte stores: 4 consecutive channels (NHWC) or 4 consecutive pixels (NCHW).
+  if (OUT_NHWC) {
+    const bool vec = (a.Cout & 3) == 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int co = m0 + (i < 4 ? ty * 4 + i : BM / 2 + ty * 4 + (i - 4));
-    if (co >= a.Cout) continue;
-    const float b = a.bias ? a.bias[co] : 0.0f;
+    for (int h = 0; h < 2; ++h) {
+      const int co = m0 + h * (BM / 2) + ty * 4;
+      if (co >= a.Cout) continue;
+      float bv[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
-      if (p >= a.P) continue;
-      const float y = (float)((double)acc[i][j] * a.scale) + b;
-      if (OUT_NHWC) {
-        a.out[p * a.Cout + co] = y;
-      } else {
-        const int64_t img = p / HoWo;
-        a.out[(img * a.Cout + co) * HoWo + (p - img * HoWo)] = y;
+      for (int i = 0; i < 4; ++i) bv[i] = (a.bias && co + i < a.Cout) ? a.bias[co + i] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
+        if (p >= a.P) continue;
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[h * 4 + i][j] * a.scale) + bv[i];
+        float* dst = a.out + p * a.Cout + co;
+        if (vec) {
+          *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (co + i < a.Cout) dst[i] = y[i];
+        }
+      }
+    }
+  } else {
+    const bool vec = (HoWo & 3) == 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int co = m0 + (i < 4 ? ty * 4 + i : BM / 2 + ty * 4 + (i - 4));
+      if (co >= a.Cout) continue;
+      const float b = a.bias ? a.bias[co] : 0.0f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t p0 = n0 + h * (BN / 2) + tx * 4;
+        float y[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = (float)((double)acc[i][h * 4 + j] * a.scale) + b;
+        if (vec && p0 + 3 < a.P) {
+          const int64_t img = p0 / HoWo;
+          *reinterpret_cast<float4*>(a.out + (img * a.Cout + co) * HoWo + (p0 - img * HoWo)) =
+              make_float4(y[0], y[1], y[2], y[3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t p = p0 + j;
+            if (p >= a.P) continue;
+            const int64_t img = p / HoWo;
+            a.out[(img * a.Cout + co) * HoWo + (p - img * HoWo)] = y[j];
+          }
+        }
       }
     }
   }
@@ -257,13 +304,13 @@ hipError_t launch_conv2d_tp(const ConvArgs& a, int out_nhwc, hipStream_t stream)
   if (a.P == 0 || a.Cout == 0) return hipSuccess;
   const int bm = conv_tile_m(a.Cout);
   if (bm == 64) {
-    const dim3 grid((unsigned)((a.P + 255) / 256), (unsigned)((a.Cout + 63) / 64));
+    const dim3 grid((unsigned)(((a.P + 255) / 256) * ((a.Cout + 63) / 64)));
     if (out_nhwc)
       conv2d_tp_kernel<64, 256, true><<<grid, kConvThreads, 0, stream>>>(a);
     else
       conv2d_tp_kernel<64, 256, false><<<grid, kConvThreads, 0, stream>>>(a);
   } else {
-    const dim3 grid((unsigned)((a.P + 127) / 128), (unsigned)((a.Cout + 127) / 128));
+    const dim3 grid((unsigned)(((a.P + 127) / 128) * ((a.Cout + 127) / 128)));
     if (out_nhwc)
       conv2d_tp_kernel<128, 128, true><<<grid, kConvThreads, 0, stream>>>(a);
     else

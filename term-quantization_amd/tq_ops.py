@@ -9,6 +9,7 @@
 Errors mirror the reference boundary (kernels/tr_cuda.cpp:12-18): RuntimeError for a non-CUDA
 or non-contiguous input, a RuntimeError for an unsupported dtype, IndexError for < 2 dims.
 """
+import numpy as np
 import torch
 
 import tq_native
@@ -16,6 +17,19 @@ import tq_native
 ACT_CHANNEL_ALIGN = 8   # int16 codes per 16-byte vector
 K_ALIGN = 32            # codes per K-step of the term-pair kernel
 MAX_CODE_BITS = 14      # |code| <= 2^bitwidth must fit int16
+
+_kernel_hook = None
+
+
+def set_kernel_hook(hook):
+    """Install ``hook(name, work, launch_fn)`` around the term-pair path's kernel launches
+    (bench.py times them with HIP events on the launch stream); None removes it."""
+    global _kernel_hook
+    _kernel_hook = hook
+
+
+def _launch(name, work, fn):
+    return fn() if _kernel_hook is None else _kernel_hook(name, work, fn)
 
 
 def _check_input(input):
@@ -131,15 +145,17 @@ def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_chan
     ho = conv_out_size(h, kh, stride[0], padding[0], dilation[0])
     wo = conv_out_size(w, kw, stride[1], padding[1], dilation[1])
     codes = torch.empty((n, h, w, cp), dtype=torch.int16, device=x.device)
-    tq_native.act_encode(x, nhwc, float(sf_x), int(data_bits), int(data_terms), codes)
+    _launch("act_encode", 4 * n * c * h * w + 2 * n * h * w * cp,
+            lambda: tq_native.act_encode(x, nhwc, float(sf_x), int(data_bits), int(data_terms),
+                                         codes))
     fmt = torch.channels_last if nhwc else torch.contiguous_format
     out = torch.empty((n, out_channels, ho, wo), dtype=torch.float32, device=x.device,
                       memory_format=fmt)
     # one rounding of the exact integer sum: scale = fp32(sf_x) * fp32(sf_w) in double
-    scale = float(torch.tensor(sf_x, dtype=torch.float32)) * float(
-        torch.tensor(sf_w, dtype=torch.float32))
+    scale = float(np.float32(sf_x)) * float(np.float32(sf_w))
     if bias is not None:
         bias = bias.detach().to(torch.float32).contiguous()
-    tq_native.conv2d_termpair(codes, w_packed, out_channels, kh, kw, stride, padding, dilation,
-                              scale, bias, out, nhwc)
+    _launch("conv2d_termpair", n * ho * wo * out_channels * c * kh * kw,
+            lambda: tq_native.conv2d_termpair(codes, w_packed, out_channels, kh, kw, stride,
+                                              padding, dilation, scale, bias, out, nhwc))
     return out
