@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
 
 import cnn_models  # noqa: E402
 import profile_model  # noqa: E402
+import tq_fuse  # noqa: E402
 import tq_ops  # noqa: E402
 import tr_layer  # noqa: E402
 import util  # noqa: E402
@@ -48,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=24,
                     help="images in the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unfused", action="store_true",
+                    help="run the module path (separate BN/ReLU/add/TR passes) instead of "
+                         "the fused executor")
     return ap.parse_args()
 
 
@@ -155,6 +159,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     model_fp, qmodel, tmacs_per_img = build_model(dev, args.batch, rank)
+    runner = qmodel if args.unfused else tq_fuse.FusedResNet(qmodel)
 
     # resident synthetic inputs (two batches, alternated) and labels
     data = util.SyntheticImageNet(2 * args.batch, args.batch, seed=rank, device=dev)
@@ -167,7 +172,7 @@ def main():
 
     def step(i):
         x, y = batches[i % 2]
-        out = qmodel(x)
+        out = runner(x)
         counters[0] += (out.argmax(1) == y).sum()
         counters[1] += y.numel()
 
@@ -228,7 +233,10 @@ def main():
             "config": {"workload": "resnet18-tq-g8-k12 (wb=db=9, dt=3), synthetic N(0,1) "
                                    "3x224x224, random-init weights",
                        "per_gpu_batch": args.batch, "global_batch": args.batch * world,
-                       "parallelism": "dp%d (batch-sharded, no data-path collective)" % world},
+                       "parallelism": "dp%d (batch-sharded, no data-path collective)" % world,
+                       "executor": "module path" if args.unfused else
+                                   "fused (BN/ReLU/residual/next-layer TR in the conv "
+                                   "epilogue)"},
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,
             "roofline": {

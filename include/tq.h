@@ -97,6 +97,54 @@ int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w
                        float *out, int64_t ho, int64_t wo, int32_t out_nhwc, void *stream);
 
 /*
+ * Fused epilogue of tq_conv2d_termpair_fused (channels_last output only).  Per output
+ * (pixel p, channel c), with acc the exact integer term-pair sum:
+ *   y = fp32(acc * ch_scale[c] + ch_shift[c])          if ch_scale (conv scale, bias and an
+ *                                                       eval-mode BatchNorm folded, fp64)
+ *     = fp32(acc * scale + bias[c])                    otherwise (plain conv)
+ *   y = y + residual[p][c]            (fp32, if residual; [P][cout] channels_last)
+ *   y = max(y, 0)                     (if relu)
+ *   out[p][c] = y                     (if out)
+ *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   int16, [P][cp_a] (if codes_a)
+ *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   int16, [P][cp_b] (if codes_b)
+ * codes_a/_b are the next TR layers' activation codes (tr_layer.py:96-99 applied to y), so
+ * those layers skip their own activation pass.  cp_* = roundup(cout, 8); cout % 4 == 0.
+ */
+typedef struct tq_conv_epilogue {
+  const double *ch_scale;
+  const double *ch_shift;
+  const float *residual;
+  int32_t relu;
+  int16_t *codes_a;
+  int64_t cp_a;
+  float sf_a;
+  int32_t bits_a;
+  int32_t terms_a;
+  int16_t *codes_b;
+  int64_t cp_b;
+  float sf_b;
+  int32_t bits_b;
+  int32_t terms_b;
+  /* execution choices: config 0 = built-in heuristic, 1..tq_conv2d_num_configs() = a fixed
+   * tile configuration; split_k > 1 (with config != 0) or the heuristic may split the K
+   * loop over workgroups, which needs `workspace` (int32, n*ho*wo*cout elements; zeroed by
+   * the call) -- without a workspace the K loop is never split */
+  int32_t *workspace;
+  int32_t split_k;
+  int32_t config;
+} tq_conv_epilogue;
+
+/* Number of tile configurations selectable through tq_conv_epilogue.config. */
+int32_t tq_conv2d_num_configs(void);
+
+int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int64_t w,
+                             int64_t cp, const int16_t *w_codes, int64_t cout, int64_t kh,
+                             int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
+                             int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                             double scale, const float *bias, float *out, int64_t ho,
+                             int64_t wo, const tq_conv_epilogue *epi, void *stream);
+
+/*
  * Batched activation-scale calibration, replacing the 2048-launch loop of
  * tr_layer.mse_profile (tr_layer.py:43-54):
  *   errs[s] = sum_b hist[b] * (x[b] - TR(x[b]; sf = sfs[s], bitwidth, group 1, k))^2

@@ -118,11 +118,17 @@ int tq_act_encode(const float* x, int32_t in_nhwc, int64_t n, int64_t c, int64_t
 
 int64_t tq_conv2d_cout_align(void) { return 128; }
 
-int tq_conv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t cp,
-                       const int16_t* w_codes, int64_t cout, int64_t kh, int64_t kw, int64_t kp,
-                       int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
-                       int64_t dil_h, int64_t dil_w, double scale, const float* bias,
-                       float* out, int64_t ho, int64_t wo, int32_t out_nhwc, void* stream) {
+int32_t tq_conv2d_num_configs(void) { return tq::conv_num_configs(); }
+
+}  // extern "C"
+
+namespace {
+
+int conv_common(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t cp,
+                const int16_t* w_codes, int64_t cout, int64_t kh, int64_t kw, int64_t kp,
+                int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                int64_t dil_h, int64_t dil_w, double scale, const float* bias, float* out,
+                int64_t ho, int64_t wo, tq::ConvArgs* a) {
   if (n < 0 || h < 1 || w < 1 || cout < 1 || kh < 1 || kw < 1)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad shape");
   if (cp < 8 || cp % 8 != 0)
@@ -140,30 +146,108 @@ int tq_conv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: code buffers must be 16-byte aligned");
   if (n * h * w * cp >= (int64_t)1 << 40 || cout > (1 << 24) || kp > (1 << 24))
     return fail(TQ_ERR_UNSUPPORTED, "conv2d: problem too large");
+  *a = tq::ConvArgs();
+  a->x = act_codes;
+  a->w = w_codes;
+  a->bias = bias;
+  a->out = out;
+  a->P = n * ho * wo;
+  a->N = (int)n;
+  a->H = (int)h;
+  a->W = (int)w;
+  a->Cp = (int)cp;
+  a->Cout = (int)cout;
+  a->KH = (int)kh;
+  a->KW = (int)kw;
+  a->sh = (int)stride_h;
+  a->sw = (int)stride_w;
+  a->ph = (int)pad_h;
+  a->pw = (int)pad_w;
+  a->dh = (int)dil_h;
+  a->dw = (int)dil_w;
+  a->Ho = (int)ho;
+  a->Wo = (int)wo;
+  a->Kp = (int)kp;
+  a->scale = scale;
+  return TQ_OK;
+}
+
+int code_target(int16_t* codes, int64_t cp, float sf, int32_t bits, int32_t terms,
+                int64_t cout, const char* which) {
+  if (codes == nullptr) return TQ_OK;
+  if (cp < cout || cp % 8 != 0 || (uintptr_t)codes % 8 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d epilogue: codes_%s needs cp >= cout, "
+                "cp %% 8 == 0 and 8-byte alignment", which);
+  if (bits < 0 || bits > 14)
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d epilogue: codes_%s bitwidth must be <= 14", which);
+  if (!(sf >= 0.0f))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d epilogue: codes_%s sf must be >= 0", which);
+  return TQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tq_conv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t cp,
+                       const int16_t* w_codes, int64_t cout, int64_t kh, int64_t kw, int64_t kp,
+                       int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                       int64_t dil_h, int64_t dil_w, double scale, const float* bias,
+                       float* out, int64_t ho, int64_t wo, int32_t out_nhwc, void* stream) {
   tq::ConvArgs a;
-  a.x = act_codes;
-  a.w = w_codes;
-  a.bias = bias;
-  a.out = out;
-  a.P = n * ho * wo;
-  a.N = (int)n;
-  a.H = (int)h;
-  a.W = (int)w;
-  a.Cp = (int)cp;
-  a.Cout = (int)cout;
-  a.KH = (int)kh;
-  a.KW = (int)kw;
-  a.sh = (int)stride_h;
-  a.sw = (int)stride_w;
-  a.ph = (int)pad_h;
-  a.pw = (int)pad_w;
-  a.dh = (int)dil_h;
-  a.dw = (int)dil_w;
-  a.Ho = (int)ho;
-  a.Wo = (int)wo;
-  a.Kp = (int)kp;
-  a.scale = scale;
+  int rc = conv_common(act_codes, n, h, w, cp, w_codes, cout, kh, kw, kp, stride_h, stride_w,
+                       pad_h, pad_w, dil_h, dil_w, scale, bias, out, ho, wo, &a);
+  if (rc != TQ_OK) return rc;
+  if (out == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: out is null");
   return hip_status(tq::launch_conv2d_tp(a, out_nhwc, (hipStream_t)stream), "conv2d launch");
+}
+
+int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int64_t w,
+                             int64_t cp, const int16_t* w_codes, int64_t cout, int64_t kh,
+                             int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
+                             int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                             double scale, const float* bias, float* out, int64_t ho,
+                             int64_t wo, const tq_conv_epilogue* epi, void* stream) {
+  tq::ConvArgs a;
+  int rc = conv_common(act_codes, n, h, w, cp, w_codes, cout, kh, kw, kp, stride_h, stride_w,
+                       pad_h, pad_w, dil_h, dil_w, scale, bias, out, ho, wo, &a);
+  if (rc != TQ_OK) return rc;
+  if (epi == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: epilogue is null");
+  if (cout % 4 != 0)
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d fused epilogue needs cout %% 4 == 0");
+  if ((epi->ch_scale == nullptr) != (epi->ch_shift == nullptr))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: ch_scale and ch_shift go together");
+  if (out == nullptr && epi->codes_a == nullptr && epi->codes_b == nullptr)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: no output requested");
+  if ((out && (uintptr_t)out % 16) || (epi->residual && (uintptr_t)epi->residual % 16))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: out/residual must be 16-byte aligned");
+  rc = code_target(epi->codes_a, epi->cp_a, epi->sf_a, epi->bits_a, epi->terms_a, cout, "a");
+  if (rc != TQ_OK) return rc;
+  rc = code_target(epi->codes_b, epi->cp_b, epi->sf_b, epi->bits_b, epi->terms_b, cout, "b");
+  if (rc != TQ_OK) return rc;
+  a.ch_scale = epi->ch_scale;
+  a.ch_shift = epi->ch_shift;
+  a.residual = epi->residual;
+  a.relu = epi->relu;
+  a.codes_a = epi->codes_a;
+  a.cp_a = (int)epi->cp_a;
+  a.sf_a = epi->sf_a;
+  a.maxv_a = (float)((1u << (epi->codes_a ? epi->bits_a : 0)) - 1u);
+  a.k_a = epi->terms_a < 0 ? 0 : epi->terms_a;
+  a.codes_b = epi->codes_b;
+  a.cp_b = (int)epi->cp_b;
+  a.sf_b = epi->sf_b;
+  a.maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
+  a.k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
+  if (epi->config < 0 || epi->config > tq::conv_num_configs() || epi->split_k < 0 ||
+      epi->split_k > 64)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
+  if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: workspace must be 16-byte aligned");
+  a.config = epi->config;
+  a.splits = epi->split_k;
+  a.ws = epi->workspace;
+  return hip_status(tq::launch_conv2d_tp(a, 1, (hipStream_t)stream), "conv2d launch");
 }
 
 int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,

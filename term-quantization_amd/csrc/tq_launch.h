@@ -20,6 +20,25 @@ struct ConvArgs {
   int64_t P;            // N * Ho * Wo
   int N, H, W, Cp, Cout, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo, Kp;
   double scale;         // double(sf_x) * double(sf_w)
+  // Fused epilogue (channels_last output only; all optional):
+  //   y = fp32(acc * ch_scale[c] + ch_shift[c])   (per-channel: conv scale, bias, folded BN)
+  //       else fp32(acc * scale + bias[c])
+  //   y = y + residual[p][c] (fp32);  y = max(y, 0) if relu
+  //   out[p][c] = y (if out);  codes_a/b[p][c] = TR(y; sf, bits, k) (next layers' inputs)
+  const double* ch_scale;
+  const double* ch_shift;
+  const float* residual;
+  int relu;
+  int16_t* codes_a;
+  int cp_a, k_a;
+  float sf_a, maxv_a;
+  int16_t* codes_b;
+  int cp_b, k_b;
+  float sf_b, maxv_b;
+  // Execution choices: config 0 = heuristic, 1..conv_num_configs() = a fixed tile config;
+  // splits = K-splits for that config (needs ws: int32 [P][Cout] workspace, NHWC output).
+  int config, splits;
+  int* ws;
 };
 
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
@@ -27,6 +46,7 @@ hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, 
                              hipStream_t stream);
 
 int conv_tile_m(int64_t cout);
+int conv_num_configs();
 
 hipError_t launch_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                               int64_t nsf, int bitwidth, int k, double* errs, hipStream_t stream);

@@ -26,19 +26,89 @@ namespace tq {
 
 namespace {
 
-constexpr int kConvThreads = 256;
-
 __device__ __forceinline__ int dot2(int a, int b, int c) {
   typedef short s2 __attribute__((ext_vector_type(2)));
   return __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, a), __builtin_bit_cast(s2, b), c, false);
 }
 
-template <int BM, int BN, bool OUT_NHWC>
-__global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) {
+// Per-channel epilogue coefficients of channels co..co+3: y = acc * sc + sh (fp64).
+__device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4],
+                                          double sh[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = co + i < a.Cout;
+    if (a.ch_scale) {
+      sc[i] = ok ? a.ch_scale[co + i] : 0.0;
+      sh[i] = ok ? a.ch_shift[co + i] : 0.0;
+    } else {
+      sc[i] = a.scale;
+      sh[i] = (a.bias && ok) ? (double)a.bias[co + i] : 0.0;
+    }
+  }
+}
+
+__device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, int co,
+                                             const float y[4], float sf, float maxv, int k) {
+  int32_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = tr_value_g1(y[i], sf, maxv, k);
+  *reinterpret_cast<int2*>(codes + p * cp + co) =
+      make_int2((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16));
+}
+
+// Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
+// one fp64->fp32 rounding, residual add and ReLU in fp32, fp32 store, next layers' TR codes
+// (tr_layer.py:96-99 applied to the stored value).
+__device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
+                                           const int acc[4], const double sc[4],
+                                           const double sh[4], bool vec) {
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
+  if (a.residual) {
+    const float* r = a.residual + p * a.Cout + co;
+    if (vec) {
+      const float4 rv = *reinterpret_cast<const float4*>(r);
+      y[0] += rv.x;
+      y[1] += rv.y;
+      y[2] += rv.z;
+      y[3] += rv.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (co + i < a.Cout) y[i] += r[i];
+    }
+  }
+  if (a.relu) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+  }
+  if (a.out) {
+    float* dst = a.out + p * a.Cout + co;
+    if (vec) {
+      *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (co + i < a.Cout) dst[i] = y[i];
+    }
+  }
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.sf_a, a.maxv_a, a.k_a);
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.sf_b, a.maxv_b, a.k_b);
+}
+
+// Implicit-GEMM term-pair conv.  BM x BN output tile (Cout x pixels), THREADS lanes with an
+// 8 x 8 int32 accumulator tile each.  SPLIT: this block sums only its share of the K-steps
+// and adds its partial sums into the int32 workspace (exact, order-independent);
+// conv_finalize_kernel applies the epilogue afterwards.
+template <int BM, int BN, int THREADS, bool OUT_NHWC, bool SPLIT, int OCC>
+__global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
   constexpr int TX = BN / 8;
-  static_assert((BM / 8) * TX == kConvThreads, "8x8 per thread");
-  constexpr int A_LOADS = BM * 4 / kConvThreads;  // 16-B vectors per thread per K-step
-  constexpr int B_LOADS = BN * 4 / kConvThreads;
+  static_assert((BM / 8) * TX == THREADS, "8x8 accumulators per thread");
+  constexpr int ROWS = THREADS / 4;                // rows (m or n) per load slot
+  constexpr int A_LOADS = BM / ROWS;               // 16-B vectors per thread per K-step
+  constexpr int B_LOADS = BN / ROWS;
+  static_assert(A_LOADS >= 1 && B_LOADS >= 1, "tile too small for the thread count");
 
   __shared__ __attribute__((aligned(16))) int32_t As[2][16][BM];
   __shared__ __attribute__((aligned(16))) int32_t Bs[2][16][BN];
@@ -46,31 +116,36 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
   const int tid = threadIdx.x;
   const int tx = tid % TX;
   const int ty = tid / TX;
-  // XCD-aware tile order: blocks are dealt round-robin to the 8 XCDs (bid % 8), so give
-  // each XCD a contiguous run of logical tiles, Cout tiles of one pixel tile adjacent --
-  // neighbouring pixel tiles share halo rows and all Cout tiles share the activation tile,
-  // and both then hit the same XCD's L2.  Bijective for any grid size.
+  // XCD-aware work order: blocks are dealt round-robin to the 8 XCDs (bid % 8), so each XCD
+  // gets a contiguous run of logical work items -- the K-splits and Cout tiles of one pixel
+  // tile adjacent, neighbouring pixel tiles next -- and halo rows / shared activation tiles
+  // hit one L2.  Bijective for any grid size (placement is a speed choice only).
   const int nblk = gridDim.x;
   const int bid = blockIdx.x;
   const int q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int item = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int splits = SPLIT ? a.splits : 1;
+  const int split = item % splits;
+  const int tile = item / splits;
   const int mt = (a.Cout + BM - 1) / BM;
   const int m0 = (tile % mt) * BM;
   const int64_t n0 = (int64_t)(tile / mt) * BN;
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  const int nsteps_all = a.Kp / 32;
+  const int ks_begin = (int)((int64_t)split * nsteps_all / splits);
+  const int nsteps = (int)((int64_t)(split + 1) * nsteps_all / splits) - ks_begin;
 
-  // Load-slot geometry: a 16-B vector = 8 int16 codes = 4 k-pairs.  Lanes 0-15 of a
-  // 16-lane quarter take 16 rows (pixels) at the same k-vector v, so one ds_write_b32
-  // instruction touches at most 2 lanes per bank.
+  // Load-slot geometry: a 16-B vector = 8 int16 codes = 4 k-pairs.  Lanes 0-15 of each
+  // 16-lane quarter take 16 rows at the same k-vector v, so one ds_write_b32 instruction
+  // puts at most 2 lanes on a bank.
   const int v = (tid >> 4) & 3;
-  const int rowl = (tid & 15) + 16 * (tid >> 6);  // + 64*r for slot r
+  const int rowl = (tid & 15) + 16 * (tid >> 6);
 
-  // Activation slots: per-pixel origin and row base.
   int64_t pbase[B_LOADS];
   int ih0[B_LOADS], iw0[B_LOADS];
 #pragma unroll
   for (int r = 0; r < B_LOADS; ++r) {
-    const int64_t p = n0 + rowl + 64 * r;
+    const int64_t p = n0 + rowl + ROWS * r;
     if (p < a.P) {
       const int64_t img = p / HoWo;
       const int64_t rem = p - img * HoWo;
@@ -85,25 +160,22 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
       pbase[r] = 0;
     }
   }
-  // k-vector state of this lane (shared by all its activation slots)
-  int kc = v * 8;  // channel within tap
-  int kr = 0, ks = 0, ktap = 0;
-  while (kc >= a.Cp) {
-    kc -= a.Cp;
-    ++ktap;
-    if (++ks == a.KW) {
-      ks = 0;
-      ++kr;
-    }
+  // this lane's k-vector position: k = (kr*KW + ks)*Cp + kc
+  int ktap, kc, kr, ks;
+  {
+    const int k0 = ks_begin * 32 + v * 8;
+    ktap = k0 / a.Cp;
+    kc = k0 - ktap * a.Cp;
+    kr = ktap / a.KW;
+    ks = ktap - kr * a.KW;
   }
 
   const int16_t* __restrict__ wrow[A_LOADS];
 #pragma unroll
   for (int r = 0; r < A_LOADS; ++r)
-    wrow[r] = a.w + (int64_t)(m0 + rowl + 64 * r) * a.Kp + v * 8;
+    wrow[r] = a.w + (int64_t)(m0 + rowl + ROWS * r) * a.Kp + (int64_t)ks_begin * 32 + v * 8;
 
   const int ntaps = a.KH * a.KW;
-  const int nsteps = a.Kp / 32;
 
   int4 ra[A_LOADS], rb[B_LOADS];
   auto load_tile = [&](int step) {
@@ -134,7 +206,7 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int r = 0; r < A_LOADS; ++r) {
-      const int m = rowl + 64 * r;
+      const int m = rowl + ROWS * r;
       As[buf][v * 4 + 0][m] = ra[r].x;
       As[buf][v * 4 + 1][m] = ra[r].y;
       As[buf][v * 4 + 2][m] = ra[r].z;
@@ -142,7 +214,7 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
     }
 #pragma unroll
     for (int r = 0; r < B_LOADS; ++r) {
-      const int n = rowl + 64 * r;
+      const int n = rowl + ROWS * r;
       Bs[buf][v * 4 + 0][n] = rb[r].x;
       Bs[buf][v * 4 + 1][n] = rb[r].y;
       Bs[buf][v * 4 + 2][n] = rb[r].z;
@@ -156,8 +228,10 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = 0;
 
-  load_tile(0);
-  store_tile(0);
+  if (nsteps > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
   __syncthreads();
 
   for (int step = 0; step < nsteps; ++step) {
@@ -180,32 +254,42 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
     __syncthreads();
   }
 
-  // Epilogue: one rounding of the exact integer sum, then bias (fp32, as conv + bias).
-  // 16-byte stores: 4 consecutive channels (NHWC) or 4 consecutive pixels (NCHW).
+  if (SPLIT) {
+    // exact int32 partial sums into the workspace ([P][Cout], zeroed by the launcher)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int co = m0 + h * (BM / 2) + ty * 4;
+      if (co >= a.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
+        if (p >= a.P) continue;
+        int* dst = a.ws + p * a.Cout + co;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (co + i < a.Cout) atomicAdd(dst + i, acc[h * 4 + i][j]);
+      }
+    }
+    return;
+  }
+
+  // Epilogue: one rounding of the exact integer sum (fp64 scale/shift), 16-byte stores of 4
+  // consecutive channels (NHWC) or 4 consecutive pixels (NCHW).
   if (OUT_NHWC) {
     const bool vec = (a.Cout & 3) == 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int co = m0 + h * (BM / 2) + ty * 4;
       if (co >= a.Cout) continue;
-      float bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = (a.bias && co + i < a.Cout) ? a.bias[co + i] : 0.0f;
+      double sc[4], sh[4];
+      load_coef(a, co, sc, sh);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
         if (p >= a.P) continue;
-        float y[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[h * 4 + i][j] * a.scale) + bv[i];
-        float* dst = a.out + p * a.Cout + co;
-        if (vec) {
-          *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (co + i < a.Cout) dst[i] = y[i];
-        }
+        const int acc4[4] = {acc[h * 4][j], acc[h * 4 + 1][j], acc[h * 4 + 2][j],
+                             acc[h * 4 + 3][j]};
+        emit4_nhwc(a, p, co, acc4, sc, sh, vec);
       }
     }
   } else {
@@ -214,13 +298,14 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
     for (int i = 0; i < 8; ++i) {
       const int co = m0 + (i < 4 ? ty * 4 + i : BM / 2 + ty * 4 + (i - 4));
       if (co >= a.Cout) continue;
-      const float b = a.bias ? a.bias[co] : 0.0f;
+      const double sc = a.scale;
+      const double sh = a.bias ? (double)a.bias[co] : 0.0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int64_t p0 = n0 + h * (BN / 2) + tx * 4;
         float y[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = (float)((double)acc[i][h * 4 + j] * a.scale) + b;
+        for (int j = 0; j < 4; ++j) y[j] = (float)((double)acc[i][h * 4 + j] * sc + sh);
         if (vec && p0 + 3 < a.P) {
           const int64_t img = p0 / HoWo;
           *reinterpret_cast<float4*>(a.out + (img * a.Cout + co) * HoWo + (p0 - img * HoWo)) =
@@ -237,6 +322,20 @@ __global__ __launch_bounds__(kConvThreads, 3) void conv2d_tp_kernel(ConvArgs a) 
       }
     }
   }
+}
+
+// Split-K epilogue: 4 channels of one pixel per lane from the int32 workspace.
+__global__ __launch_bounds__(256) void conv_finalize_kernel(ConvArgs a) {
+  const int groups = a.Cout / 4;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= a.P * groups) return;
+  const int64_t p = t / groups;
+  const int co = (int)(t - p * groups) * 4;
+  const int4 s = *reinterpret_cast<const int4*>(a.ws + p * a.Cout + co);
+  const int acc4[4] = {s.x, s.y, s.z, s.w};
+  double sc[4], sh[4];
+  load_coef(a, co, sc, sh);
+  emit4_nhwc(a, p, co, acc4, sc, sh, true);
 }
 
 // TR of fp32 activations straight into int16 NHWC codes (group_size 1, the reference's
@@ -298,24 +397,77 @@ hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, 
   return hipGetLastError();
 }
 
+// Tile configurations: {BM, BN, threads}.  All keep 8 x 8 accumulators per lane.
+struct TileCfg {
+  int bm, bn, threads;
+};
+constexpr TileCfg kTileCfgs[] = {{128, 128, 256}, {64, 256, 256}, {64, 128, 128},
+                                 {128, 64, 128},  {128, 128, 256}, {64, 256, 256}};
+// configs 4 and 5 repeat 0 and 1 with a 4-waves-per-SIMD register budget (128 VGPRs)
+constexpr int kNumTileCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
+
 int conv_tile_m(int64_t cout) { return cout <= 64 ? 64 : 128; }
 
-hipError_t launch_conv2d_tp(const ConvArgs& a, int out_nhwc, hipStream_t stream) {
-  if (a.P == 0 || a.Cout == 0) return hipSuccess;
-  const int bm = conv_tile_m(a.Cout);
-  if (bm == 64) {
-    const dim3 grid((unsigned)(((a.P + 255) / 256) * ((a.Cout + 63) / 64)));
-    if (out_nhwc)
-      conv2d_tp_kernel<64, 256, true><<<grid, kConvThreads, 0, stream>>>(a);
-    else
-      conv2d_tp_kernel<64, 256, false><<<grid, kConvThreads, 0, stream>>>(a);
+int conv_num_configs() { return kNumTileCfgs; }
+
+namespace {
+
+// Heuristic for config 0: 64-row tiles for Cout <= 64; otherwise 128x128, split over K
+// while the grid leaves CUs idle (fewer than ~3 resident 4-wave blocks per CU) and each
+// split keeps >= 8 K-steps.
+void pick_config(const ConvArgs& a, int out_nhwc, int* cfg, int* splits) {
+  if (a.config > 0 && a.config <= kNumTileCfgs) {
+    *cfg = a.config - 1;
+    *splits = a.splits > 0 ? a.splits : 1;
   } else {
-    const dim3 grid((unsigned)(((a.P + 127) / 128) * ((a.Cout + 127) / 128)));
-    if (out_nhwc)
-      conv2d_tp_kernel<128, 128, true><<<grid, kConvThreads, 0, stream>>>(a);
-    else
-      conv2d_tp_kernel<128, 128, false><<<grid, kConvThreads, 0, stream>>>(a);
+    *cfg = a.Cout <= 64 ? 1 : 0;
+    *splits = 1;
+    const TileCfg& t = kTileCfgs[*cfg];
+    const int64_t tiles = ((a.P + t.bn - 1) / t.bn) * ((a.Cout + t.bm - 1) / t.bm);
+    const int nsteps = a.Kp / 32;
+    while (tiles * *splits < 2 * 256 * 3 && nsteps / (*splits * 2) >= 8 && *splits < 8)
+      *splits *= 2;
   }
+  if (!out_nhwc || !a.ws || (a.Cout & 3)) *splits = 1;  // split-K only for NHWC outputs
+}
+
+template <int BM, int BN, int T, int OCC>
+hipError_t launch_cfg(const ConvArgs& a, int out_nhwc, int splits, hipStream_t stream) {
+  const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + BM - 1) / BM);
+  const dim3 grid((unsigned)(tiles * splits));
+  if (splits > 1)
+    conv2d_tp_kernel<BM, BN, T, true, true, OCC><<<grid, T, 0, stream>>>(a);
+  else if (out_nhwc)
+    conv2d_tp_kernel<BM, BN, T, true, false, OCC><<<grid, T, 0, stream>>>(a);
+  else
+    conv2d_tp_kernel<BM, BN, T, false, false, OCC><<<grid, T, 0, stream>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_conv2d_tp(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
+  if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
+  ConvArgs a = a_in;
+  int cfg, splits;
+  pick_config(a, out_nhwc, &cfg, &splits);
+  a.splits = splits;
+  if (splits > 1) {
+    hipError_t e = hipMemsetAsync(a.ws, 0, (size_t)a.P * a.Cout * sizeof(int32_t), stream);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e;
+  switch (cfg) {
+    case 0: e = launch_cfg<128, 128, 256, 3>(a, out_nhwc, splits, stream); break;
+    case 1: e = launch_cfg<64, 256, 256, 3>(a, out_nhwc, splits, stream); break;
+    case 2: e = launch_cfg<64, 128, 128, 3>(a, out_nhwc, splits, stream); break;
+    case 3: e = launch_cfg<128, 64, 128, 3>(a, out_nhwc, splits, stream); break;
+    case 4: e = launch_cfg<128, 128, 256, 4>(a, out_nhwc, splits, stream); break;
+    default: e = launch_cfg<64, 256, 256, 4>(a, out_nhwc, splits, stream); break;
+  }
+  if (e != hipSuccess || splits == 1) return e;
+  const int64_t n = a.P * (a.Cout / 4);
+  conv_finalize_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,147 @@
+"""Fused TQ executor for a converted, calibrated ResNet (BasicBlock) model.
+
+The module path (torchvision-style ResNet with TRConv2dLayer, BatchNorm2d, ReLU modules) runs
+every op as its own pass over HBM: term-pair conv -> BN -> ReLU -> (+identity -> ReLU) ->
+the next layer's activation TR.  This executor runs the same math with each block's ops
+folded into the term-pair kernel's epilogue (tq_conv2d_termpair_fused):
+
+  conv1:       codes(x; sf1)   -> TR(relu(bn1(conv1)); sf2) as int16 codes   (no fp32 tensor)
+  downsample:  codes(x; sf_d)  -> bn_d(conv_d) fp32                          (the identity)
+  conv2:       codes(mid; sf2) -> y = relu(bn2(conv2) + identity) fp32, plus
+                                  TR(y; sf of the next block's conv1 / downsample) codes
+
+so between the stem and the classifier only the term-pair kernels touch HBM.  BatchNorm is
+folded per channel in fp64 (eval mode: y*gamma/sqrt(var+eps) + beta - mean*gamma/sqrt(..)),
+the sum rounds to fp32 once, the residual add and ReLU are fp32 as in the module path, and
+each activation code is TR of exactly that fp32 value (tr_layer.py:96-99), so the executor
+matches the module path to fp32 rounding of the BN (DESIGN.md "Fused executor").
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+import tq_native
+import tq_ops
+import tr_layer
+
+
+def _fold_bn(layer, bn):
+    """Per-channel (scale, shift) in fp64: bn(acc * s + bias) == acc * scale + shift."""
+    dev = layer.w_codes.device
+    s = float(np.float32(layer.input_quant.sf)) * float(np.float32(layer.w_sf))
+    bias = (layer.conv.bias.detach().double() if layer.conv.bias is not None
+            else torch.zeros(layer.conv.out_channels, dtype=torch.float64, device=dev))
+    if bn is None:
+        return (torch.full_like(bias, s), bias.clone())
+    a = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    scale = s * a
+    shift = (bias - bn.running_mean.detach().double()) * a + bn.bias.detach().double()
+    return scale.contiguous(), shift.contiguous()
+
+
+class _Conv(object):
+    """One TRConv2dLayer prepared for the fused kernel."""
+
+    def __init__(self, layer, bn):
+        if not isinstance(layer, tr_layer.TRConv2dLayer) or not layer.termpair:
+            raise ValueError("fused executor needs term-pair TRConv2dLayer convolutions")
+        if layer.input_quant.tracking:
+            raise ValueError("calibrate first: set_tr_tracking(model, False)")
+        c = layer.conv
+        self.layer = layer
+        self.cout = c.out_channels
+        self.kh, self.kw = c.kernel_size
+        self.stride, self.padding, self.dilation = c.stride, c.padding, c.dilation
+        self.cp_in = layer.act_channels
+        self.quant = (layer.input_quant.sf, layer.data_bits, layer.data_terms)
+        self.scale, self.shift = _fold_bn(layer, bn)
+        if self.cout % 4:
+            raise ValueError("fused epilogue needs Cout % 4 == 0")
+
+    def out_hw(self, h, w):
+        return (tq_ops.conv_out_size(h, self.kh, self.stride[0], self.padding[0],
+                                     self.dilation[0]),
+                tq_ops.conv_out_size(w, self.kw, self.stride[1], self.padding[1],
+                                     self.dilation[1]))
+
+    def __call__(self, codes, out=None, residual=None, relu=False, next_a=None, next_b=None):
+        n, h, w, _ = codes.shape
+        ho, wo = self.out_hw(h, w)
+        dev = codes.device
+        ca = cb = None
+        if next_a is not None:
+            ca = torch.empty((n, ho, wo, next_a.cp_in), dtype=torch.int16, device=dev)
+        if next_b is not None:
+            cb = torch.empty((n, ho, wo, next_b.cp_in), dtype=torch.int16, device=dev)
+        if out is True:
+            out = torch.empty((n, self.cout, ho, wo), dtype=torch.float32, device=dev,
+                              memory_format=torch.channels_last)
+        res = None
+        if residual is not None:
+            res = residual if residual.is_contiguous(memory_format=torch.channels_last) \
+                else residual.contiguous(memory_format=torch.channels_last)
+        cin = self.layer.conv.in_channels
+        ws = torch.empty(n * ho * wo * self.cout, dtype=torch.int32, device=dev)
+        tq_ops._launch(
+            "conv2d_termpair", n * ho * wo * self.cout * cin * self.kh * self.kw,
+            lambda: tq_native.conv2d_termpair_fused(
+                codes, self.layer.w_codes, self.cout, self.kh, self.kw, self.stride,
+                self.padding, self.dilation, ho, wo, out=out, ch_scale=self.scale,
+                ch_shift=self.shift, residual=res, relu=relu, codes_a=ca,
+                quant_a=next_a.quant if next_a else None, codes_b=cb,
+                quant_b=next_b.quant if next_b else None, workspace=ws))
+        return out, ca, cb
+
+
+class _Block(object):
+    def __init__(self, block):
+        self.conv1 = _Conv(block.conv1, block.bn1)
+        self.conv2 = _Conv(block.conv2, block.bn2)
+        self.down = None
+        if block.downsample is not None:
+            self.down = _Conv(block.downsample[0], block.downsample[1])
+
+
+class FusedResNet(nn.Module):
+    """Inference executor over a converted + calibrated torchvision-style ResNet."""
+
+    def __init__(self, qmodel):
+        super(FusedResNet, self).__init__()
+        self.qmodel = qmodel
+        self.blocks = []
+        for layer in (qmodel.layer1, qmodel.layer2, qmodel.layer3, qmodel.layer4):
+            for block in layer:
+                self.blocks.append(_Block(block))
+
+    @torch.no_grad()
+    def forward(self, x):
+        m = self.qmodel
+        x = x.contiguous(memory_format=torch.channels_last)
+        x = m.maxpool(m.relu(m.bn1(m.conv1(x))))
+        x = x.contiguous(memory_format=torch.channels_last)
+        first = self.blocks[0]
+        codes = torch.empty((x.shape[0], x.shape[2], x.shape[3], first.conv1.cp_in),
+                            dtype=torch.int16, device=x.device)
+        n, c, h, w = x.shape
+        tq_ops._launch("act_encode", 4 * x.numel() + 2 * codes.numel(),
+                       lambda: tq_native.act_encode(x, True, first.conv1.quant[0],
+                                                    first.conv1.quant[1], first.conv1.quant[2],
+                                                    codes))
+        codes_down = None
+        if first.down is not None:
+            codes_down = torch.empty_like(codes)
+            tq_native.act_encode(x, True, *first.down.quant, codes_down)
+        for i, b in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            _, mid, _ = b.conv1(codes, next_a=b.conv2)
+            if b.down is not None:
+                identity, _, _ = b.down(codes_down, out=True)
+            else:
+                identity = x
+            x, codes, codes_down = b.conv2(
+                mid, out=True, residual=identity, relu=True,
+                next_a=nxt.conv1 if nxt else None,
+                next_b=nxt.down if nxt is not None and nxt.down is not None else None)
+        x = m.avgpool(x)
+        x = torch.flatten(x, 1)
+        return m.fc(x)

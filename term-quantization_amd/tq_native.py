@@ -36,13 +36,29 @@ _SIGNATURES = {
                          _vp],
     "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _vp],
     "tq_conv2d_cout_align": [],
+    "tq_conv2d_num_configs": [],
     "tq_conv2d_termpair": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64,
                            _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32,
                            _vp],
     "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
 }
+
+class ConvEpilogue(ctypes.Structure):
+    """tq_conv_epilogue (include/tq.h)."""
+    _fields_ = [("ch_scale", _vp), ("ch_shift", _vp), ("residual", _vp), ("relu", _i32),
+                ("codes_a", _vp), ("cp_a", _i64), ("sf_a", _f32), ("bits_a", _i32),
+                ("terms_a", _i32),
+                ("codes_b", _vp), ("cp_b", _i64), ("sf_b", _f32), ("bits_b", _i32),
+                ("terms_b", _i32),
+                ("workspace", _vp), ("split_k", _i32), ("config", _i32)]
+
+
+_SIGNATURES["tq_conv2d_termpair_fused"] = [
+    _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+    _i64, _f64, _vp, _vp, _i64, _i64, ctypes.POINTER(ConvEpilogue), _vp]
+
 _RESTYPE = {"tq_version": ctypes.c_char_p, "tq_last_error": ctypes.c_char_p,
-            "tq_conv2d_cout_align": _i64}
+            "tq_conv2d_cout_align": _i64, "tq_conv2d_num_configs": _i32}
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 
@@ -140,3 +156,29 @@ def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
                                   int(bitwidth), int(num_keep_terms), _ptr(errs), _stream(x))
     _check(rc)
     return errs
+
+
+def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilation, ho, wo,
+                          out=None, ch_scale=None, ch_shift=None, residual=None, relu=False,
+                          codes_a=None, quant_a=None, codes_b=None, quant_b=None,
+                          workspace=None, split_k=0, config=0):
+    """Term-pair conv with the fused epilogue of tq_conv2d_termpair_fused (channels_last).
+    quant_a/_b = (sf, bits, terms) of the layer consuming codes_a/_b.  ``workspace`` (int32,
+    >= n*ho*wo*cout elements) lets the kernel split the K loop over workgroups."""
+    n, h, w, cp = codes.shape
+    epi = ConvEpilogue()
+    epi.ch_scale, epi.ch_shift = _ptr(ch_scale), _ptr(ch_shift)
+    epi.residual, epi.relu = _ptr(residual), int(bool(relu))
+    if codes_a is not None:
+        epi.codes_a, epi.cp_a = _ptr(codes_a), codes_a.shape[-1]
+        epi.sf_a, epi.bits_a, epi.terms_a = float(quant_a[0]), int(quant_a[1]), int(quant_a[2])
+    if codes_b is not None:
+        epi.codes_b, epi.cp_b = _ptr(codes_b), codes_b.shape[-1]
+        epi.sf_b, epi.bits_b, epi.terms_b = float(quant_b[0]), int(quant_b[1]), int(quant_b[2])
+    epi.workspace, epi.split_k, epi.config = _ptr(workspace), int(split_k), int(config)
+    with torch.cuda.device(codes.device):
+        rc = lib().tq_conv2d_termpair_fused(
+            _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1], stride[0],
+            stride[1], padding[0], padding[1], dilation[0], dilation[1], 0.0, None, _ptr(out),
+            ho, wo, ctypes.byref(epi), _stream(codes))
+    _check(rc)

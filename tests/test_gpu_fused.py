@@ -1,0 +1,87 @@
+"""GPU parity of the fused term-pair epilogue (BN fold, residual, ReLU, next-layer TR codes)
+and of the fused ResNet executor against the module path."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import oracle
+import tq_fuse
+import tq_native
+import tr_layer
+import cnn_models
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _layer(cin, cout, k, s, seed):
+    torch.manual_seed(seed)
+    conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=False)
+    nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 9, 8, 12)
+    layer.input_quant.tracking = False
+    layer.input_quant.sf = 0.03
+    bn = nn.BatchNorm2d(cout).to(DEV).eval()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    return layer, bn
+
+
+@pytest.mark.parametrize("cfg", [(64, 64, 3, 1, 14), (64, 128, 3, 2, 15), (64, 128, 1, 2, 14),
+                                 (128, 256, 3, 1, 7)])
+def test_fused_epilogue_matches_reference_composition(cfg):
+    cin, cout, k, s, hw = cfg
+    layer, bn = _layer(cin, cout, k, s, seed=cin + k)
+    conv = tq_fuse._Conv(layer, bn)
+    nxt, _ = _layer(cout, cout, 3, 1, seed=99)
+    nxt.input_quant.sf = 0.05
+    nxt_conv = tq_fuse._Conv(nxt, None)
+    torch.manual_seed(7)
+    x = torch.relu(torch.randn(2, cin, hw, hw, device=DEV))
+    codes = torch.empty((2, hw, hw, conv.cp_in), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x.contiguous(memory_format=torch.channels_last), True, 0.03, 9, 3,
+                         codes)
+    ho, wo = conv.out_hw(hw, hw)
+    res = torch.randn(2, cout, ho, wo, device=DEV).contiguous(memory_format=torch.channels_last)
+    y, ca, _ = conv(codes, out=True, residual=res, relu=True, next_a=nxt_conv)
+    # reference composition in fp64 from the oracle's TR'd tensors
+    xq = torch.from_numpy(oracle.tr(x.cpu().numpy().reshape(1, -1, 1, 1), 0.03, 9, 1,
+                                    3)).view(x.shape).double()
+    wq = layer.conv.weight.detach().cpu().double()
+    z = F.conv2d(xq, wq, None, s, k // 2)
+    mag = F.conv2d(xq.abs(), wq.abs(), None, s, k // 2)
+    a = (bn.weight.detach().double() / torch.sqrt(bn.running_var.double() + bn.eps)).cpu()
+    bnz = (z - bn.running_mean.double().cpu().view(1, -1, 1, 1)) * a.view(1, -1, 1, 1) + \
+        bn.bias.detach().double().cpu().view(1, -1, 1, 1)
+    ref = torch.relu(bnz + res.double().cpu())
+    bound = 1e-5 * (torch.maximum(ref.abs(), mag * a.abs().view(1, -1, 1, 1)) +
+                    res.double().abs().cpu()) + 1e-30
+    assert bool(((y.double().cpu() - ref).abs() <= bound).all())
+    # the emitted codes are exactly TR of the fp32 output the kernel wrote
+    yq = oracle.tr(y.contiguous().cpu().numpy().reshape(1, -1, 1, 1), 0.05, 9, 1, 3)
+    exp_codes = np.rint(yq.reshape(y.shape) / np.float32(0.05)).astype(np.int64)
+    got = ca.cpu().long()[..., :cout].permute(0, 3, 1, 2)
+    assert torch.equal(got, torch.from_numpy(exp_codes))
+
+
+def test_fused_resnet_matches_module_path():
+    torch.manual_seed(0)
+    model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        q(x)
+    tr_layer.set_tr_tracking(q, False)
+    fused = tq_fuse.FusedResNet(q)
+    with torch.no_grad():
+        ref = q(x)
+        got = fused(x)
+    rel = (got - ref).norm() / ref.norm()
+    assert rel.item() < 1e-3, rel.item()
+    assert (got.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.75

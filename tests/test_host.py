@@ -204,3 +204,47 @@ def test_compute_compressed_hese_matches_python_loop():
     exp = (int(np.ceil(np.log2(8))) + 2) * sum(oracle.tr_layer_hese_len(v)
                                                for v in q.view(-1).tolist())
     assert bits == exp
+
+
+def test_mnist_mlp_counts_match_published(stub_tr):
+    import evaluate_mlp
+    from train_mlp import MNISTMLP
+    torch.manual_seed(0)
+    x = torch.randn(1, 1, 28, 28)
+    pub_q = PUBLISHED["mnist-quant.json"]
+    for i, wb in enumerate([2, 3, 4, 5, 6]):  # evaluate_mlp.sh:3 (g=1, wt=wb, db=dt=6)
+        m = MNISTMLP()
+        st = evaluate_mlp.static_linear_layer_settings(m, wb, 1, wb)
+        q = evaluate_mlp.replace_linear_layers(m, st, 6, 6)
+        tmacs, bits = profile_model.get_model_ops(q, (x,))
+        assert tmacs == pub_q["tmacs"][i] and bits == pub_q["param_bits"][i]
+    pub_t = PUBLISHED["mnist-tr.json"]
+    for i, wt in enumerate([6, 8, 10, 12, 14]):  # evaluate_mlp.sh:4 (wb=4, g=16, db=dt=6)
+        m = MNISTMLP()
+        st = evaluate_mlp.static_linear_layer_settings(m, 4, 16, wt)
+        q = evaluate_mlp.replace_linear_layers(m, st, 6, 6)
+        tmacs, _ = profile_model.get_model_ops(q, (x,))
+        assert tmacs == pub_t["tmacs"][i]
+
+
+def test_lstm_counts_match_published(stub_tr):
+    """Decoder-only term-pair MACs of one 35x10 batch and the g=1 parameter bits of the
+    LSTM-650 sweeps (evaluate_lstm.sh), fp32-accumulated like thop."""
+    import evaluate_lstm
+    from lstm_models.model import RNNModel
+    torch.manual_seed(0)
+    model = RNNModel("LSTM", evaluate_lstm.WT2_VOCAB, 650, 650, 2, 0.5, True)
+    data = torch.randint(0, evaluate_lstm.WT2_VOCAB, (35, 10))
+    inputs = (data, model.init_hidden(10))
+    pub_q = PUBLISHED["lstm-quant.json"]
+    for i, wb in enumerate([5, 6, 7, 8, 9]):
+        st = evaluate_lstm.static_lstm_layer_settings(model, wb, 1, wb)
+        q = evaluate_lstm.convert_model(model, st, 8, 8)
+        tmacs, bits = profile_model.get_model_ops(q, inputs)
+        assert tmacs == pub_q["tmacs"][i] and bits == pub_q["param_bits"][i]
+    pub_t = PUBLISHED["lstm-tr.json"]
+    for i, wt in enumerate([8, 12, 16, 20, 24]):
+        st = evaluate_lstm.static_lstm_layer_settings(model, 8, 8, wt)
+        q = evaluate_lstm.convert_model(model, st, 8, 8)
+        tmacs, _ = profile_model.get_model_ops(q, inputs)
+        assert tmacs == pub_t["tmacs"][i]

@@ -43,6 +43,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true",
+                    help="time every tile config x K-split per layer (fused NHWC entry)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -88,6 +90,52 @@ def main():
             i + 1, cin, cout, k, s, hin, hin, t * 1e6, mac / t / 1e12))
     print("conv total: %.2f ms  %.1f TMAC/s  -> %.0f img/s (convs only)" % (
         total_t * 1e3, total_mac / total_t / 1e12, args.batch / total_t))
+    if args.sweep:
+        sweep(args, dev)
+
+
+def sweep(args, dev):
+    ncfg = tq_native.lib().tq_conv2d_num_configs()
+    best_total = 0.0
+    auto_total = 0.0
+    seen = {}
+    for i, (cin, cout, k, s, hin) in enumerate(RESNET18_TR):
+        key = (cin, cout, k, s, hin)
+        if key in seen:
+            best_total += seen[key][0]
+            auto_total += seen[key][1]
+            continue
+        conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(dev)
+        layer = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+        cp = tq_ops.act_channels(cin)
+        xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
+            memory_format=torch.channels_last)
+        codes = torch.empty((args.batch, hin, hin, cp), dtype=torch.int16, device=dev)
+        tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
+        ho = (hin + 2 * (k // 2) - k) // s + 1
+        o = torch.empty((args.batch, cout, ho, ho), device=dev,
+                        memory_format=torch.channels_last)
+        ws = torch.empty(args.batch * ho * ho * cout, dtype=torch.int32, device=dev)
+        sc = torch.full((cout,), 1e-4, dtype=torch.float64, device=dev)
+        sh = torch.zeros(cout, dtype=torch.float64, device=dev)
+        mac = args.batch * cout * ho * ho * cin * k * k
+        res = {}
+        for cfg in range(0, ncfg + 1):
+            for sp in ([1, 2, 3, 4, 6, 8] if cfg else [0]):
+                fn = lambda: tq_native.conv2d_termpair_fused(
+                    codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho,
+                    out=o, ch_scale=sc, ch_shift=sh, workspace=ws, split_k=sp, config=cfg)
+                res[(cfg, sp)] = time_fn(fn, max(5, args.iters // 2))
+        best = min(res, key=res.get)
+        auto = res[(0, 0)]
+        seen[key] = (res[best], auto)
+        best_total += res[best]
+        auto_total += auto
+        line = " ".join("c%ds%d=%.0f" % (c, sp, t * 1e6) for (c, sp), t in sorted(res.items()))
+        print("sweep conv%02d %s best=c%ds%d %.1f us (%.1f TMAC/s) auto %.1f us | %s" % (
+            i + 1, key, best[0], best[1], res[best] * 1e6, mac / res[best] / 1e12, auto * 1e6,
+            line))
+    print("sweep totals: best %.2f ms, auto %.2f ms" % (best_total * 1e3, auto_total * 1e3))
 
 
 if __name__ == "__main__":
