@@ -412,9 +412,11 @@ int conv_num_configs() { return kNumTileCfgs; }
 
 namespace {
 
-// Heuristic for config 0: 64-row tiles for Cout <= 64; otherwise 128x128, split over K
-// while the grid leaves CUs idle (fewer than ~3 resident 4-wave blocks per CU) and each
-// split keeps >= 8 K-steps.
+// Heuristic for config 0, from the per-layer sweep of tools/microbench.py --sweep on MI355X
+// (profiles/r01_sweep.txt): 64x256 tiles for Cout <= 64, else 128x128, one K pass; only when
+// the 128x128 grid leaves most CUs with < 2 tiles and K is deep (ResNet-18 layer4 3x3) does
+// a 3-way K split of 128x64 tiles pay for its int32 atomics (~12 %).  Splitting any larger
+// grid costs more in atomics than it gains (2-4x slower at layer1).
 void pick_config(const ConvArgs& a, int out_nhwc, int* cfg, int* splits) {
   if (a.config > 0 && a.config <= kNumTileCfgs) {
     *cfg = a.config - 1;
@@ -422,11 +424,12 @@ void pick_config(const ConvArgs& a, int out_nhwc, int* cfg, int* splits) {
   } else {
     *cfg = a.Cout <= 64 ? 1 : 0;
     *splits = 1;
-    const TileCfg& t = kTileCfgs[*cfg];
-    const int64_t tiles = ((a.P + t.bn - 1) / t.bn) * ((a.Cout + t.bm - 1) / t.bm);
+    const int64_t tiles128 = ((a.P + 127) / 128) * ((a.Cout + 127) / 128);
     const int nsteps = a.Kp / 32;
-    while (tiles * *splits < 2 * 256 * 3 && nsteps / (*splits * 2) >= 8 && *splits < 8)
-      *splits *= 2;
+    if (a.Cout > 64 && tiles128 < 2 * 256 && nsteps >= 96) {
+      *cfg = 3;
+      *splits = 3;
+    }
   }
   if (!out_nhwc || !a.ws || (a.Cout & 3)) *splits = 1;  // split-K only for NHWC outputs
 }

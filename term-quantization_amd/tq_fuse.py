@@ -133,7 +133,7 @@ class FusedResNet(nn.Module):
             tq_native.act_encode(x, True, *first.down.quant, codes_down)
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
-            _, mid, _ = b.conv1(codes, next_a=b.conv2)
+            _, mid, _ = b.conv1(codes, relu=True, next_a=b.conv2)
             if b.down is not None:
                 identity, _, _ = b.down(codes_down, out=True)
             else:
