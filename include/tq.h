@@ -145,6 +145,24 @@ int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int
                              int64_t wo, const tq_conv_epilogue *epi, void *stream);
 
 /*
+ * Depthwise term-pair Conv2d (groups == C_in == C_out): per output channel c,
+ *   out = fp32(sum_{taps} act_codes[.., c] * w_codes[tap][c] * scale) + bias[c]
+ * exactly in int32 before the one rounding -- the reference's `self.conv(xq)` for the
+ * depthwise layers of MobileNet-V2 / EfficientNet-b0 (16-bit weights: int32 codes).
+ *   act_codes  [n][h][w][cp] int16 (tq_act_encode), cp % 8 == 0, 16-byte aligned
+ *   w_codes    [kh*kw][cp] int32, tap-major, channel fastest, pad channels 0, 16-byte aligned
+ *   out        [n][ho][wo][c] (out_nhwc = 1) or [n][c][ho][wo]
+ * Taps outside the input read 0, so pad_top / pad_left plus (ho, wo) express symmetric and
+ * TensorFlow-style asymmetric "same" padding alike.  The caller guarantees
+ * max_c sum_tap |w_codes| * max|act_code| < 2^31 and |act_code| < 2^23, |w_code| < 2^23.
+ */
+int tq_dwconv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w, int64_t c,
+                         int64_t cp, const int32_t *w_codes, int64_t kh, int64_t kw,
+                         int64_t stride_h, int64_t stride_w, int64_t pad_top, int64_t pad_left,
+                         int64_t dil_h, int64_t dil_w, double scale, const float *bias,
+                         float *out, int64_t ho, int64_t wo, int32_t out_nhwc, void *stream);
+
+/*
  * Batched activation-scale calibration, replacing the 2048-launch loop of
  * tr_layer.mse_profile (tr_layer.py:43-54):
  *   errs[s] = sum_b hist[b] * (x[b] - TR(x[b]; sf = sfs[s], bitwidth, group 1, k))^2

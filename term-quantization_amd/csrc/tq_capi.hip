@@ -250,6 +250,49 @@ int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int
   return hip_status(tq::launch_conv2d_tp(a, 1, (hipStream_t)stream), "conv2d launch");
 }
 
+int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t c,
+                         int64_t cp, const int32_t* w_codes, int64_t kh, int64_t kw,
+                         int64_t stride_h, int64_t stride_w, int64_t pad_top, int64_t pad_left,
+                         int64_t dil_h, int64_t dil_w, double scale, const float* bias,
+                         float* out, int64_t ho, int64_t wo, int32_t out_nhwc, void* stream) {
+  if (n < 0 || h < 1 || w < 1 || c < 1 || kh < 1 || kw < 1 || ho < 1 || wo < 1)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: bad shape");
+  if (cp < c || cp % 8 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: cp must be >= c and a multiple of 8");
+  if (stride_h < 1 || stride_w < 1 || dil_h < 1 || dil_w < 1 || pad_top < 0 || pad_left < 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: bad stride/padding/dilation");
+  if ((uintptr_t)act_codes % 16 != 0 || (uintptr_t)w_codes % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: code buffers must be 16-byte aligned");
+  if (out_nhwc && c % 8 == 0 && (uintptr_t)out % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: out must be 16-byte aligned");
+  if (n * h * w * cp >= (int64_t)1 << 40 || kh * kw > 4096)
+    return fail(TQ_ERR_UNSUPPORTED, "dwconv2d: problem too large");
+  if (out == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: out is null");
+  tq::DwConvArgs a;
+  a.x = act_codes;
+  a.w = w_codes;
+  a.bias = bias;
+  a.out = out;
+  a.N = (int)n;
+  a.H = (int)h;
+  a.W = (int)w;
+  a.C = (int)c;
+  a.Cp = (int)cp;
+  a.KH = (int)kh;
+  a.KW = (int)kw;
+  a.sh = (int)stride_h;
+  a.sw = (int)stride_w;
+  a.ph = (int)pad_top;
+  a.pw = (int)pad_left;
+  a.dh = (int)dil_h;
+  a.dw = (int)dil_w;
+  a.Ho = (int)ho;
+  a.Wo = (int)wo;
+  a.out_nhwc = out_nhwc ? 1 : 0;
+  a.scale = scale;
+  return hip_status(tq::launch_dwconv_tp(a, (hipStream_t)stream), "dwconv2d launch");
+}
+
 int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                    int64_t nsf, int32_t bitwidth, int32_t num_keep_terms, double* errs,
                    void* stream) {

@@ -41,6 +41,17 @@ struct ConvArgs {
   int* ws;
 };
 
+struct DwConvArgs {
+  const int16_t* x;     // activation codes [N][H][W][Cp]
+  const int32_t* w;     // weight codes [KH*KW][Cp] (channel fastest)
+  const float* bias;    // [C] or nullptr
+  float* out;           // [N][Ho][Wo][C] (out_nhwc) or [N][C][Ho][Wo]
+  int N, H, W, C, Cp, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo, out_nhwc;
+  double scale;
+};
+
+hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream);
+
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
                              int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,
                              hipStream_t stream);

@@ -1,0 +1,93 @@
+// Depthwise term-pair Conv2d (groups == C_in == C_out) for MobileNet-V2 / EfficientNet-b0,
+// whose depthwise layers keep (16, 1, 16) settings (cnn_models/__init__.py:57-58): 16-bit
+// weight term sums do not fit int16, so weights stay int32 and each product is one
+// v_mad_i32_i24 (|v_x| <= 2^14, |v_w| <= 2^16, both inside 24-bit operands; a 7x7 window
+// sums to < 2^37 only for 16+14 bits -- the host checks the int32 bound).
+//
+// One lane per (output pixel, 8 channels): KH*KW 16-byte activation-code loads (NHWC, the
+// 8 channels of one tap are contiguous), 8 int32 weights per tap from the [KH*KW][C] weight
+// table (L1/L2-resident), exact int32 sums, one rounding in the epilogue.  HBM-bound: the
+// activation tile is re-read from cache per tap, the output written once.
+// Padding is implicit (any tap outside the input reads 0), so asymmetric "same" padding
+// (Conv2dStaticSamePadding) is expressed by pad_top / pad_left and the output size.
+#include "tq_device.h"
+#include "tq_launch.h"
+
+namespace tq {
+
+namespace {
+
+// Operands known to fit 24 signed bits let the compiler emit v_mad_i32_i24 (full rate).
+__device__ __forceinline__ int sext24(int v) { return (v << 8) >> 8; }
+
+__global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
+  const int chunks = a.Cp / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+  if (t >= P * chunks) return;
+  const int64_t p = t / chunks;
+  const int c0 = (int)(t - p * chunks) * 8;
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  const int64_t img = p / HoWo;
+  const int rem = (int)(p - img * HoWo);
+  const int oh = rem / a.Wo;
+  const int ow = rem - oh * a.Wo;
+  int acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0;
+  for (int r = 0; r < a.KH; ++r) {
+    const int ih = oh * a.sh - a.ph + r * a.dh;
+    if (ih < 0 || ih >= a.H) continue;
+    for (int s = 0; s < a.KW; ++s) {
+      const int iw = ow * a.sw - a.pw + s * a.dw;
+      if (iw < 0 || iw >= a.W) continue;
+      const int4 xv =
+          *reinterpret_cast<const int4*>(a.x + ((img * a.H + ih) * a.W + iw) * a.Cp + c0);
+      const int32_t* wt = a.w + (int64_t)(r * a.KW + s) * a.Cp + c0;
+      const int4 w0 = *reinterpret_cast<const int4*>(wt);
+      const int4 w1 = *reinterpret_cast<const int4*>(wt + 4);
+      const int xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      const int ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int lo = (int)(short)(xs[i] & 0xFFFF);
+        const int hi = xs[i] >> 16;
+        acc[2 * i] += lo * sext24(ws[2 * i]);
+        acc[2 * i + 1] += hi * sext24(ws[2 * i + 1]);
+      }
+    }
+  }
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    const double sh = (a.bias && c < a.C) ? (double)a.bias[c] : 0.0;
+    y[i] = (float)((double)acc[i] * a.scale + sh);
+  }
+  if (a.out_nhwc) {
+    float* dst = a.out + p * a.C + c0;
+    if ((a.C & 7) == 0) {
+      *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(y[4], y[5], y[6], y[7]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (c0 + i < a.C) dst[i] = y[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (c0 + i < a.C) a.out[(img * a.C + c0 + i) * HoWo + rem] = y[i];
+  }
+}
+
+}  // namespace
+
+hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
+  const int64_t n = (int64_t)a.N * a.Ho * a.Wo * (a.Cp / 8);
+  if (n == 0) return hipSuccess;
+  dwconv_tp_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace tq

@@ -41,6 +41,8 @@ _SIGNATURES = {
                            _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32,
                            _vp],
     "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
+    "tq_dwconv2d_termpair": [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
+                             _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32, _vp],
 }
 
 class ConvEpilogue(ctypes.Structure):
@@ -182,3 +184,17 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
             stride[1], padding[0], padding[1], dilation[0], dilation[1], 0.0, None, _ptr(out),
             ho, wo, ctypes.byref(epi), _stream(codes))
     _check(rc)
+
+
+def dwconv2d_termpair(codes, c, w_codes, kh, kw, stride, pad_tl, dilation, scale, bias, out,
+                      out_nhwc):
+    """Depthwise term-pair conv (tq_dwconv2d_termpair); w_codes int32 [kh*kw, cp]."""
+    n, h, w, cp = codes.shape
+    ho, wo = out.shape[2], out.shape[3]
+    with torch.cuda.device(codes.device):
+        rc = lib().tq_dwconv2d_termpair(_ptr(codes), n, h, w, c, cp, _ptr(w_codes), kh, kw,
+                                        stride[0], stride[1], pad_tl[0], pad_tl[1],
+                                        dilation[0], dilation[1], float(scale), _ptr(bias),
+                                        _ptr(out), ho, wo, int(out_nhwc), _stream(codes))
+    _check(rc)
+    return out

@@ -159,3 +159,68 @@ def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_chan
             lambda: tq_native.conv2d_termpair(codes, w_packed, out_channels, kh, kw, stride,
                                               padding, dilation, scale, bias, out, nhwc))
     return out
+
+
+def static_padding(conv):
+    """(top, bottom, left, right) zero padding a Conv2dStaticSamePadding-style module applies
+    before its convolution (efficientnet_pytorch semantics), else zeros."""
+    pad = getattr(conv, "static_padding", None)
+    if pad is None or not isinstance(pad, torch.nn.ZeroPad2d):
+        return (0, 0, 0, 0)
+    left, right, top, bottom = pad.padding
+    return (top, bottom, left, right)
+
+
+def pack_dw_weight(codes):
+    """[C, 1, KH, KW] int32 term sums -> int32 [KH*KW, Cp] (tap-major, channel fastest)."""
+    c, _, kh, kw = codes.shape
+    cp = act_channels(c)
+    packed = torch.zeros((kh * kw, cp), dtype=torch.int32, device=codes.device)
+    packed[:, :c] = codes.reshape(c, kh * kw).t()
+    return packed.contiguous(), cp
+
+
+def tr_dwconv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, channels,
+                kernel_size, stride, padding, dilation, pad_tblr=(0, 0, 0, 0)):
+    """Depthwise conv2d(TR(x), TR(w)) + bias by exact term-pair accumulation."""
+    if not x.is_cuda:
+        raise RuntimeError("input must be a CUDA tensor")
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("tr_dwconv2d: expects a 4-D float32 input")
+    n, c, h, w = x.shape
+    if c != channels:
+        raise RuntimeError("tr_dwconv2d: input has %d channels, weights expect %d" % (c,
+                                                                                  channels))
+    nhwc = (not x.is_contiguous()) and x.is_contiguous(memory_format=torch.channels_last)
+    if not nhwc and not x.is_contiguous():
+        x = x.contiguous()
+    kh, kw = kernel_size
+    top, bottom, left, right = pad_tblr
+    ho = conv_out_size(h + top + bottom, kh, stride[0], padding[0], dilation[0])
+    wo = conv_out_size(w + left + right, kw, stride[1], padding[1], dilation[1])
+    codes = torch.empty((n, h, w, cp), dtype=torch.int16, device=x.device)
+    _launch("act_encode", 4 * n * c * h * w + 2 * n * h * w * cp,
+            lambda: tq_native.act_encode(x, nhwc, float(sf_x), int(data_bits), int(data_terms),
+                                         codes))
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    out = torch.empty((n, c, ho, wo), dtype=torch.float32, device=x.device, memory_format=fmt)
+    scale = float(np.float32(sf_x)) * float(np.float32(sf_w))
+    if bias is not None:
+        bias = bias.detach().to(torch.float32).contiguous()
+    _launch("dwconv2d_termpair", n * ho * wo * c * kh * kw,
+            lambda: tq_native.dwconv2d_termpair(codes, c, w_packed, kh, kw, stride,
+                                                (top + padding[0], left + padding[1]),
+                                                dilation, scale, bias, out, nhwc))
+    return out
+
+
+def tr_linear(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features):
+    """linear(TR(x), TR(w)) + bias by exact term-pair accumulation: the rows of x are the
+    pixels of a 1x1 term-pair conv (channels_last [M, C, 1, 1] is x's own memory)."""
+    shape = x.shape
+    x2 = x.reshape(-1, shape[-1]).contiguous()
+    m = x2.shape[0]
+    xc = x2.view(m, 1, 1, shape[-1]).permute(0, 3, 1, 2)  # channels_last view, no copy
+    y = tr_conv2d(xc, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features,
+                  (1, 1), (1, 1), (0, 0), (1, 1))
+    return y.permute(0, 2, 3, 1).reshape(*shape[:-1], out_features)

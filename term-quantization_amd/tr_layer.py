@@ -153,13 +153,15 @@ class TRConv2dLayer(nn.Module):
     Construction TRs the weight with group size ``group_size`` and budget ``num_terms`` and
     keeps the fake-quantized tensor as ``self.conv.weight`` (so ``profile_model`` and any
     caller reading the weight see the reference values).  It also keeps the integer term
-    sums, packed for the term-pair kernel, in the ``w_codes`` buffer.
+    sums, packed for the term-pair kernels, in the ``w_codes`` buffer.
 
     forward: while tracking, ``self.conv`` on the unquantized input (the reference returns x
-    from the quantizer while tracking); afterwards ``tr_conv2d`` -- conv2d(TR(x), TR(w)) + bias
-    by exact term-pair accumulation -- when the layer fits the term-pair kernel (groups 1,
-    data/weight bits <= 14, zero padding), else the reference's own composition
-    ``self.conv(self.input_quant(x))`` with the HIP TR op (``self.termpair`` says which)."""
+    from the quantizer while tracking); afterwards conv2d(TR(x), TR(w)) + bias by exact
+    term-pair accumulation -- ``self.mode``:
+      "termpair"   groups == 1, data/weight bits <= 14 (int16 codes): tq_ops.tr_conv2d
+      "depthwise"  groups == C_in == C_out, weight bits <= 22: tq_ops.tr_dwconv2d
+      "reference"  anything else: the reference composition self.conv(self.input_quant(x))
+                   with the HIP TR op (``self.termpair`` is True only for "termpair")."""
 
     def __init__(self, conv_layer, data_bits=8, data_terms=4, weight_bits=8,
                  group_size=1, num_terms=8):
@@ -173,33 +175,52 @@ class TRConv2dLayer(nn.Module):
         self.weight_bits = weight_bits
         w = conv_layer.weight
         self.w_sf = _w_sf(w, weight_bits)
-        self.termpair = (conv_layer.groups == 1 and weight_bits <= tq_ops.MAX_CODE_BITS
-                         and data_bits <= tq_ops.MAX_CODE_BITS
-                         and getattr(conv_layer, 'padding_mode', 'zeros') == 'zeros'
-                         and not isinstance(conv_layer.padding, str)
-                         and w.dtype == torch.float32)
-        if self.termpair:
+        c = conv_layer
+        plain = (getattr(c, 'padding_mode', 'zeros') == 'zeros'
+                 and not isinstance(c.padding, str) and w.dtype == torch.float32
+                 and data_bits <= tq_ops.MAX_CODE_BITS)
+        mode = "reference"
+        if plain and c.groups == 1 and weight_bits <= tq_ops.MAX_CODE_BITS:
+            mode = "termpair"
+        elif (plain and c.groups > 1 and c.groups == c.in_channels == c.out_channels
+              and weight_bits <= 22):
+            mode = "depthwise"
+        packed = None
+        if mode != "reference":
             wq, codes = tq_ops.tr_encode(w.detach().contiguous(), self.w_sf, weight_bits,
                                          group_size, num_terms)
-            packed, cp = tq_ops.pack_conv_weight(codes)
             # int32 accumulator bound: sum_k |v_w| * max|v_x| (|v_x| <= 2^data_bits)
             bound = codes.abs().to(torch.int64).flatten(1).sum(1).max().item() << data_bits
-            self.termpair = bound < 2**31
+            if bound >= 2**31:
+                mode = "reference"
+            elif mode == "termpair":
+                packed, cp = tq_ops.pack_conv_weight(codes)
+            else:
+                packed, cp = tq_ops.pack_dw_weight(codes)
         else:
             wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
-        if self.termpair:
-            self.register_buffer('w_codes', packed)
+        self.mode = mode
+        self.termpair = mode == "termpair"
+        self.register_buffer('w_codes', packed)
+        if packed is not None:
             self.act_channels = cp
-        else:
-            self.register_buffer('w_codes', None)
         conv_layer.weight = nn.Parameter(wq)
         self.conv = conv_layer
 
     def forward(self, x):
-        if self.input_quant.tracking or not self.termpair:
+        if self.input_quant.tracking or self.mode == "reference":
             xq = self.input_quant(x)
             return self.conv(xq)
         c = self.conv
+        pad = tq_ops.static_padding(c)
+        if self.mode == "depthwise":
+            return tq_ops.tr_dwconv2d(x, self.input_quant.sf, self.data_bits, self.data_terms,
+                                      self.w_codes, self.act_channels, self.w_sf, c.bias,
+                                      c.out_channels, c.kernel_size, c.stride, c.padding,
+                                      c.dilation, pad)
+        if any(pad):
+            # TR(0) == 0: zero-padding before the encode equals padding the TR'd input
+            x = torch.nn.functional.pad(x, (pad[2], pad[3], pad[0], pad[1]))
         return tq_ops.tr_conv2d(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, c.bias,
                                 c.out_channels, c.kernel_size, c.stride, c.padding, c.dilation)
@@ -217,10 +238,14 @@ class TRLinearLayer(nn.Module):
     Like the reference, forward returns ``self.linear(x)`` on the UNquantized input
     (tr_layer.py:152-154): only the weights are term-quantized.  The input quantizer still
     records its histogram while tracking; after calibration the reference computes TR(x) and
-    discards it, which this layer skips (the output is identical)."""
+    discards it, which this layer skips (the output is identical).
+
+    ``quantize_input=True`` (an addition, off by default) uses the quantized input as the
+    reference evidently intended: linear(TR(x), TR(w)) by exact term-pair accumulation
+    (the term-pair kernel as a 1x1 conv over the flattened rows)."""
 
     def __init__(self, linear_layer, data_bits=8, data_terms=4, weight_bits=8,
-                 group_size=1, num_terms=8):
+                 group_size=1, num_terms=8, quantize_input=False):
         super(TRLinearLayer, self).__init__()
         device = linear_layer.weight.device
         self.data_bits = data_bits
@@ -229,16 +254,36 @@ class TRLinearLayer(nn.Module):
         self.group_size = group_size
         self.num_terms = num_terms
         self.weight_bits = weight_bits
+        self.quantize_input = quantize_input
         w = linear_layer.weight
         self.w_sf = _w_sf(w, weight_bits)
-        w = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
-        linear_layer.weight = nn.Parameter(w)
+        self.termpair = False
+        packed = None
+        if (quantize_input and weight_bits <= tq_ops.MAX_CODE_BITS
+                and data_bits <= tq_ops.MAX_CODE_BITS and w.dtype == torch.float32):
+            wq, codes = tq_ops.tr_encode(w.detach().contiguous(), self.w_sf, weight_bits,
+                                         group_size, num_terms)
+            bound = codes.abs().to(torch.int64).sum(1).max().item() << data_bits
+            if bound < 2**31:
+                packed, self.act_channels = tq_ops.pack_conv_weight(codes[:, :, None, None])
+                self.termpair = True
+        else:
+            wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
+        self.register_buffer('w_codes', packed)
+        linear_layer.weight = nn.Parameter(wq)
         self.linear = linear_layer
 
     def forward(self, x):
         if self.input_quant.tracking:
             self.input_quant(x)
-        return self.linear(x)
+            return self.linear(x)
+        if not self.quantize_input:
+            return self.linear(x)
+        if not self.termpair:
+            return self.linear(self.input_quant(x))
+        return tq_ops.tr_linear(x, self.input_quant.sf, self.data_bits, self.data_terms,
+                                self.w_codes, self.act_channels, self.w_sf, self.linear.bias,
+                                self.linear.out_features)
 
     def tracking(self, tracking):
         if not tracking:

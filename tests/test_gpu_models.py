@@ -1,0 +1,134 @@
+"""GPU parity of the depthwise and Linear term-pair paths and of whole converted models."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import oracle
+import tr_layer
+import cnn_models
+from cnn_models.efficientnet import Conv2dStaticSamePadding
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+RTOL = 1e-5
+
+
+def _tr_x(x, sf, db, dt):
+    return torch.from_numpy(oracle.tr(x.contiguous().cpu().numpy().reshape(1, -1, 1, 1), sf,
+                                      db, 1, dt)).view(x.shape).double()
+
+
+def _check(y, ref, mag):
+    err = (y.double().cpu() - ref).abs()
+    assert bool((err <= RTOL * torch.maximum(ref.abs(), mag) + 1e-30).all()), \
+        float((err / (RTOL * torch.maximum(ref.abs(), mag) + 1e-30)).max())
+
+
+@pytest.mark.parametrize("cfg", [
+    # channels, k, stride, pad, hw, static-same (EfficientNet), bias
+    (32, 3, 1, 1, 14, False, False), (96, 3, 2, 1, 15, False, False),
+    (144, 5, 2, 0, 16, True, False), (40, 5, 1, 0, 9, True, True), (20, 3, 1, 1, 7, False, True),
+])
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_depthwise_termpair_matches_reference(cfg, channels_last):
+    c, k, s, p, hw, same, bias = cfg
+    torch.manual_seed(c + k)
+    if same:
+        conv = Conv2dStaticSamePadding(c, c, k, stride=s, groups=c, bias=bias, image_size=hw)
+    else:
+        conv = nn.Conv2d(c, c, k, s, p, groups=c, bias=bias)
+    w = conv.weight.detach().clone()
+    b = conv.bias.detach().clone() if bias else None
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 16, 1, 16)  # (16, 1, 16) dw settings
+    assert layer.mode == "depthwise"
+    layer.input_quant.tracking = False
+    layer.input_quant.sf = 0.02
+    x = torch.relu(torch.randn(2, c, hw, hw))
+    xd = x.to(DEV)
+    if channels_last:
+        xd = xd.to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = layer(xd)
+    xq = _tr_x(x, 0.02, 9, 3)
+    wq = torch.from_numpy(oracle.tr(w.numpy(), layer.w_sf, 16, 1, 16)).double()
+    assert torch.equal(layer.conv.weight.detach().cpu().double(), wq)
+    if same:
+        xq = conv.static_padding.cpu()(xq)
+    ref = F.conv2d(xq, wq, b.double() if bias else None, s, conv.padding, 1, c)
+    mag = F.conv2d(xq.abs(), wq.abs(), None, s, conv.padding, 1, c)
+    assert y.shape == ref.shape
+    _check(y, ref, mag)
+
+
+def test_linear_termpair_matches_reference():
+    torch.manual_seed(3)
+    lin = nn.Linear(650, 300)
+    w = lin.weight.detach().clone()
+    b = lin.bias.detach().clone()
+    layer = tr_layer.TRLinearLayer(lin.to(DEV), 8, 8, 8, 8, 12, quantize_input=True)
+    assert layer.termpair
+    layer.input_quant.tracking = False
+    layer.input_quant.sf = 0.01
+    x = torch.randn(35, 10, 650)
+    with torch.no_grad():
+        y = layer(x.to(DEV))
+    xq = _tr_x(x, 0.01, 8, 8)
+    wq = torch.from_numpy(oracle.tr(w.numpy(), layer.w_sf, 8, 8, 12)).double()
+    ref = xq @ wq.t() + b.double()
+    mag = xq.abs() @ wq.abs().t()
+    assert y.shape == (35, 10, 300)
+    _check(y, ref, mag)
+
+
+def test_linear_default_keeps_reference_semantics():
+    torch.manual_seed(4)
+    lin = nn.Linear(64, 16).to(DEV)
+    layer = tr_layer.TRLinearLayer(lin, 8, 4, 8, 8, 12)
+    x = torch.randn(5, 64, device=DEV)
+    with torch.no_grad():
+        layer(x)
+        tr_layer.set_tr_tracking(nn.Sequential(layer), False)
+        y = layer(x)
+    # forward returns linear(x) on the unquantized input, with TR'd weights
+    assert torch.allclose(y, F.linear(x, layer.linear.weight, layer.linear.bias))
+
+
+@pytest.mark.parametrize("arch", ["mobilenet_v2", "efficientnet_b0"])
+def test_depthwise_models_layers_match_reference_composition(arch):
+    """Every converted layer of MobileNet-V2 / EfficientNet-b0, fed the same input, matches
+    the reference composition conv(TR(x), TR(w)) in fp64 within 1e-5."""
+    torch.manual_seed(0)
+    model = getattr(cnn_models, arch)(pretrained=False).to(DEV).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3)
+    layers = [m for m in q.modules() if isinstance(m, tr_layer.TRConv2dLayer)]
+    inputs = {}
+    hooks = [m.register_forward_pre_hook(lambda m, a: inputs.__setitem__(id(m), a[0]))
+             for m in layers]
+    x = torch.randn(2, 3, 224, 224, device=DEV)
+    with torch.no_grad():
+        q(x)
+    tr_layer.set_tr_tracking(q, False)
+    modes = set()
+    for m in layers:
+        xin = inputs[id(m)]
+        modes.add(m.mode)
+        with torch.no_grad():
+            y = m(xin)
+        c = m.conv
+        xq = _tr_x(xin, m.input_quant.sf, m.data_bits, m.data_terms)
+        wq = c.weight.detach().cpu().double()
+        pad = getattr(c, "static_padding", None)
+        if pad is not None:
+            xq = pad.cpu()(xq)
+        b = c.bias.detach().cpu().double() if c.bias is not None else None
+        ref = F.conv2d(xq, wq, b, c.stride, c.padding, c.dilation, c.groups)
+        mag = F.conv2d(xq.abs(), wq.abs(), None, c.stride, c.padding, c.dilation, c.groups)
+        if m.mode == "reference":
+            continue  # fp32 torch conv of the fake-quantized tensors, as the reference
+        _check(y, ref, mag)
+    for h in hooks:
+        h.remove()
+    assert {"termpair", "depthwise"} <= modes

@@ -1,0 +1,55 @@
+"""Run one term-pair conv config repeatedly (for PMC collection / A-B timing).
+
+    python tools/conv_probe.py --layer 6 --config 1 --split 1 --iters 50
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import tq_native  # noqa: E402
+import tq_ops  # noqa: E402
+import tr_layer  # noqa: E402
+from microbench import RESNET18_TR, time_fn  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layer", type=int, default=6)
+    ap.add_argument("--config", type=int, default=0)
+    ap.add_argument("--split", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=256)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cin, cout, k, s, hin = RESNET18_TR[args.layer - 1]
+    conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(dev)
+    layer = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    cp = tq_ops.act_channels(cin)
+    xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
+        memory_format=torch.channels_last)
+    codes = torch.empty((args.batch, hin, hin, cp), dtype=torch.int16, device=dev)
+    tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
+    ho = (hin + 2 * (k // 2) - k) // s + 1
+    o = torch.empty((args.batch, cout, ho, ho), device=dev, memory_format=torch.channels_last)
+    ws = torch.empty(args.batch * ho * ho * cout, dtype=torch.int32, device=dev)
+    sc = torch.full((cout,), 1e-4, dtype=torch.float64, device=dev)
+    sh = torch.zeros(cout, dtype=torch.float64, device=dev)
+    fn = lambda: tq_native.conv2d_termpair_fused(
+        codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho, out=o,
+        ch_scale=sc, ch_shift=sh, workspace=ws, split_k=args.split, config=args.config)
+    t = time_fn(fn, args.iters)
+    mac = args.batch * cout * ho * ho * cin * k * k
+    print("layer %d cfg %d split %d: %.1f us  %.1f TMAC/s" % (args.layer, args.config,
+                                                             args.split, t * 1e6,
+                                                             mac / t / 1e12))
+
+
+if __name__ == "__main__":
+    main()
