@@ -126,13 +126,20 @@ typedef struct tq_conv_epilogue {
   int32_t bits_b;
   int32_t terms_b;
   /* execution choices: config 0 = built-in heuristic, 1..tq_conv2d_num_configs() = a fixed
-   * tile configuration; split_k > 1 (with config != 0) or the heuristic may split the K
-   * loop over workgroups, which needs `workspace` (int32, n*ho*wo*cout elements; zeroed by
-   * the call) -- without a workspace the K loop is never split */
+   * tile configuration with split_k = 1 (data-parallel), > 1 (K loop split over that many
+   * workgroups, int32 atomics) or -1 (stream-K: one resident round of workgroups sharing the
+   * tiles x K-steps evenly).  Splitting needs `workspace` (16-byte aligned scratch of
+   * `workspace_bytes` >= tq_conv2d_workspace_bytes(n*ho*wo, cout)); without one the K loop
+   * is never split. */
   int32_t *workspace;
+  int64_t workspace_bytes;
   int32_t split_k;
   int32_t config;
 } tq_conv_epilogue;
+
+/* Scratch bytes that let tq_conv2d_termpair_fused use any K-split schedule for an output of
+ * `pixels` (= n*ho*wo) x `cout` on the calling thread's current device. */
+int64_t tq_conv2d_workspace_bytes(int64_t pixels, int64_t cout);
 
 /* Number of tile configurations selectable through tq_conv_epilogue.config. */
 int32_t tq_conv2d_num_configs(void);

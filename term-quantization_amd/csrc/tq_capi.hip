@@ -120,6 +120,10 @@ int64_t tq_conv2d_cout_align(void) { return 128; }
 
 int32_t tq_conv2d_num_configs(void) { return tq::conv_num_configs(); }
 
+int64_t tq_conv2d_workspace_bytes(int64_t pixels, int64_t cout) {
+  return tq::conv_workspace_bytes(pixels, cout);
+}
+
 }  // extern "C"
 
 namespace {
@@ -239,7 +243,7 @@ int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int
   a.sf_b = epi->sf_b;
   a.maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
   a.k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
-  if (epi->config < 0 || epi->config > tq::conv_num_configs() || epi->split_k < 0 ||
+  if (epi->config < 0 || epi->config > tq::conv_num_configs() || epi->split_k < -1 ||
       epi->split_k > 64)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
   if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
@@ -247,6 +251,7 @@ int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int
   a.config = epi->config;
   a.splits = epi->split_k;
   a.ws = epi->workspace;
+  a.ws_bytes = epi->workspace ? epi->workspace_bytes : 0;
   return hip_status(tq::launch_conv2d_tp(a, 1, (hipStream_t)stream), "conv2d launch");
 }
 

@@ -36,9 +36,11 @@ struct ConvArgs {
   int cp_b, k_b;
   float sf_b, maxv_b;
   // Execution choices: config 0 = heuristic, 1..conv_num_configs() = a fixed tile config;
-  // splits = K-splits for that config (needs ws: int32 [P][Cout] workspace, NHWC output).
+  // splits: 1 data-parallel, > 1 K-split with int32 atomics into ws ([P][Cout]), -1
+  // stream-K (ws holds two BM x BN int32 slabs per resident block); NHWC output only.
   int config, splits;
   int* ws;
+  int64_t ws_bytes;
 };
 
 struct DwConvArgs {
@@ -58,6 +60,7 @@ hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, 
 
 int conv_tile_m(int64_t cout);
 int conv_num_configs();
+int64_t conv_workspace_bytes(int64_t p, int64_t cout);
 
 hipError_t launch_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                               int64_t nsf, int bitwidth, int k, double* errs, hipStream_t stream);

@@ -19,6 +19,8 @@
 // are staged through LDS as [k-pair][m] / [k-pair][n] dwords (double-buffered, one barrier
 // per K-step) and read with ds_read_b128; the next K-step's global loads are issued before
 // the current step's 1024 dot2 per lane.
+#include <cmath>
+
 #include "tq_device.h"
 #include "tq_launch.h"
 
@@ -97,44 +99,29 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
   if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.sf_b, a.maxv_b, a.k_b);
 }
 
-// Implicit-GEMM term-pair conv.  BM x BN output tile (Cout x pixels), THREADS lanes with an
-// 8 x 8 int32 accumulator tile each.  SPLIT: this block sums only its share of the K-steps
-// and adds its partial sums into the int32 workspace (exact, order-independent);
-// conv_finalize_kernel applies the epilogue afterwards.
-template <int BM, int BN, int THREADS, bool OUT_NHWC, bool SPLIT, int OCC>
-__global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
+// LDS image of one K-step (double-buffered): [k-pair][m] and [k-pair][n] dwords.
+template <int BM, int BN>
+struct TileSmem {
+  int32_t As[2][16][BM];
+  int32_t Bs[2][16][BN];
+};
+
+// Accumulate K-steps [k_begin, k_end) of output tile (m0, n0) into acc (8 Cout x 8 pixels
+// per lane).  Operands are staged through LDS, the next step's 16-B global loads are in
+// flight during the current step's 1024 dot2 per lane, one barrier per step; ends on a
+// barrier, so the LDS image may be reused by the next call.
+template <int BM, int BN, int THREADS>
+__device__ __forceinline__ void tile_mainloop(const ConvArgs& a, int m0, int64_t n0,
+                                              int k_begin, int k_end, int (&acc)[8][8],
+                                              TileSmem<BM, BN>& sm) {
   constexpr int TX = BN / 8;
-  static_assert((BM / 8) * TX == THREADS, "8x8 accumulators per thread");
-  constexpr int ROWS = THREADS / 4;                // rows (m or n) per load slot
-  constexpr int A_LOADS = BM / ROWS;               // 16-B vectors per thread per K-step
+  constexpr int ROWS = THREADS / 4;  // rows (m or n) per load slot
+  constexpr int A_LOADS = BM / ROWS;
   constexpr int B_LOADS = BN / ROWS;
-  static_assert(A_LOADS >= 1 && B_LOADS >= 1, "tile too small for the thread count");
-
-  __shared__ __attribute__((aligned(16))) int32_t As[2][16][BM];
-  __shared__ __attribute__((aligned(16))) int32_t Bs[2][16][BN];
-
   const int tid = threadIdx.x;
   const int tx = tid % TX;
   const int ty = tid / TX;
-  // XCD-aware work order: blocks are dealt round-robin to the 8 XCDs (bid % 8), so each XCD
-  // gets a contiguous run of logical work items -- the K-splits and Cout tiles of one pixel
-  // tile adjacent, neighbouring pixel tiles next -- and halo rows / shared activation tiles
-  // hit one L2.  Bijective for any grid size (placement is a speed choice only).
-  const int nblk = gridDim.x;
-  const int bid = blockIdx.x;
-  const int q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
-  const int item = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int splits = SPLIT ? a.splits : 1;
-  const int split = item % splits;
-  const int tile = item / splits;
-  const int mt = (a.Cout + BM - 1) / BM;
-  const int m0 = (tile % mt) * BM;
-  const int64_t n0 = (int64_t)(tile / mt) * BN;
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
-  const int nsteps_all = a.Kp / 32;
-  const int ks_begin = (int)((int64_t)split * nsteps_all / splits);
-  const int nsteps = (int)((int64_t)(split + 1) * nsteps_all / splits) - ks_begin;
-
   // Load-slot geometry: a 16-B vector = 8 int16 codes = 4 k-pairs.  Lanes 0-15 of each
   // 16-lane quarter take 16 rows at the same k-vector v, so one ds_write_b32 instruction
   // puts at most 2 lanes on a bank.
@@ -163,19 +150,18 @@ __global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
   // this lane's k-vector position: k = (kr*KW + ks)*Cp + kc
   int ktap, kc, kr, ks;
   {
-    const int k0 = ks_begin * 32 + v * 8;
+    const int k0 = k_begin * 32 + v * 8;
     ktap = k0 / a.Cp;
     kc = k0 - ktap * a.Cp;
     kr = ktap / a.KW;
     ks = ktap - kr * a.KW;
   }
-
   const int16_t* __restrict__ wrow[A_LOADS];
 #pragma unroll
   for (int r = 0; r < A_LOADS; ++r)
-    wrow[r] = a.w + (int64_t)(m0 + rowl + ROWS * r) * a.Kp + (int64_t)ks_begin * 32 + v * 8;
-
+    wrow[r] = a.w + (int64_t)(m0 + rowl + ROWS * r) * a.Kp + (int64_t)k_begin * 32 + v * 8;
   const int ntaps = a.KH * a.KW;
+  const int nsteps = k_end - k_begin;
 
   int4 ra[A_LOADS], rb[B_LOADS];
   auto load_tile = [&](int step) {
@@ -192,8 +178,7 @@ __global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
           rb[r] = *reinterpret_cast<const int4*>(a.x + ((pbase[r] + ih) * a.W + iw) * a.Cp + kc);
       }
     }
-    // advance this lane's k-vector by 32 codes
-    kc += 32;
+    kc += 32;  // advance this lane's k-vector by 32 codes
     while (kc >= a.Cp) {
       kc -= a.Cp;
       ++ktap;
@@ -207,42 +192,34 @@ __global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
 #pragma unroll
     for (int r = 0; r < A_LOADS; ++r) {
       const int m = rowl + ROWS * r;
-      As[buf][v * 4 + 0][m] = ra[r].x;
-      As[buf][v * 4 + 1][m] = ra[r].y;
-      As[buf][v * 4 + 2][m] = ra[r].z;
-      As[buf][v * 4 + 3][m] = ra[r].w;
+      sm.As[buf][v * 4 + 0][m] = ra[r].x;
+      sm.As[buf][v * 4 + 1][m] = ra[r].y;
+      sm.As[buf][v * 4 + 2][m] = ra[r].z;
+      sm.As[buf][v * 4 + 3][m] = ra[r].w;
     }
 #pragma unroll
     for (int r = 0; r < B_LOADS; ++r) {
       const int n = rowl + ROWS * r;
-      Bs[buf][v * 4 + 0][n] = rb[r].x;
-      Bs[buf][v * 4 + 1][n] = rb[r].y;
-      Bs[buf][v * 4 + 2][n] = rb[r].z;
-      Bs[buf][v * 4 + 3][n] = rb[r].w;
+      sm.Bs[buf][v * 4 + 0][n] = rb[r].x;
+      sm.Bs[buf][v * 4 + 1][n] = rb[r].y;
+      sm.Bs[buf][v * 4 + 2][n] = rb[r].z;
+      sm.Bs[buf][v * 4 + 3][n] = rb[r].w;
     }
   };
 
-  int acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0;
-
-  if (nsteps > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
+  if (nsteps <= 0) return;
+  load_tile(0);
+  store_tile(0);
   __syncthreads();
-
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
     if (step + 1 < nsteps) load_tile(step + 1);
 #pragma unroll 2
     for (int kk = 0; kk < 16; ++kk) {
-      const int4 a0 = *reinterpret_cast<const int4*>(&As[cur][kk][ty * 4]);
-      const int4 a1 = *reinterpret_cast<const int4*>(&As[cur][kk][BM / 2 + ty * 4]);
-      const int4 b0 = *reinterpret_cast<const int4*>(&Bs[cur][kk][tx * 4]);
-      const int4 b1 = *reinterpret_cast<const int4*>(&Bs[cur][kk][BN / 2 + tx * 4]);
+      const int4 a0 = *reinterpret_cast<const int4*>(&sm.As[cur][kk][ty * 4]);
+      const int4 a1 = *reinterpret_cast<const int4*>(&sm.As[cur][kk][BM / 2 + ty * 4]);
+      const int4 b0 = *reinterpret_cast<const int4*>(&sm.Bs[cur][kk][tx * 4]);
+      const int4 b1 = *reinterpret_cast<const int4*>(&sm.Bs[cur][kk][BN / 2 + tx * 4]);
       const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
       const int bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
@@ -253,28 +230,17 @@ __global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
     if (step + 1 < nsteps) store_tile(cur ^ 1);
     __syncthreads();
   }
+}
 
-  if (SPLIT) {
-    // exact int32 partial sums into the workspace ([P][Cout], zeroed by the launcher)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int co = m0 + h * (BM / 2) + ty * 4;
-      if (co >= a.Cout) continue;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
-        if (p >= a.P) continue;
-        int* dst = a.ws + p * a.Cout + co;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (co + i < a.Cout) atomicAdd(dst + i, acc[h * 4 + i][j]);
-      }
-    }
-    return;
-  }
-
-  // Epilogue: one rounding of the exact integer sum (fp64 scale/shift), 16-byte stores of 4
-  // consecutive channels (NHWC) or 4 consecutive pixels (NCHW).
+// Epilogue of one tile: one rounding of the exact integer sums (fp64 scale/shift), 16-byte
+// stores of 4 consecutive channels (NHWC, with the fused residual/ReLU/next-layer codes) or
+// 4 consecutive pixels (NCHW).
+template <int BM, int BN, int THREADS, bool OUT_NHWC>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int64_t n0,
+                                              const int (&acc)[8][8]) {
+  constexpr int TX = BN / 8;
+  const int tx = threadIdx.x % TX;
+  const int ty = threadIdx.x / TX;
   if (OUT_NHWC) {
     const bool vec = (a.Cout & 3) == 0;
 #pragma unroll
@@ -293,6 +259,7 @@ __global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
       }
     }
   } else {
+    const int64_t HoWo = (int64_t)a.Ho * a.Wo;
     const bool vec = (HoWo & 3) == 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -322,6 +289,152 @@ __global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
       }
     }
   }
+}
+
+// Bijective XCD-aware remap of the block index: blocks are dealt round-robin to the 8 XCDs
+// (bid % 8), so hand each XCD a contiguous run of logical work items (neighbouring pixel
+// tiles share halo rows, Cout tiles of a pixel tile share its activation tile, both then
+// hit one L2).  Placement is a speed choice only.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// Data-parallel schedule: one tile (or one K-split of a tile) per block.  SPLIT: the block
+// adds its partial sums into the int32 workspace (exact, order-independent) and
+// conv_finalize_kernel applies the epilogue.
+template <int BM, int BN, int THREADS, bool OUT_NHWC, bool SPLIT, int OCC>
+__global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_kernel(ConvArgs a) {
+  static_assert((BM / 8) * (BN / 8) == THREADS, "8x8 accumulators per thread");
+  __shared__ __attribute__((aligned(16))) TileSmem<BM, BN> sm;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int splits = SPLIT ? a.splits : 1;
+  const int split = item % splits;
+  const int tile = item / splits;
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int m0 = (tile % mt) * BM;
+  const int64_t n0 = (int64_t)(tile / mt) * BN;
+  const int nsteps_all = a.Kp / 32;
+  const int k_begin = (int)((int64_t)split * nsteps_all / splits);
+  const int k_end = (int)((int64_t)(split + 1) * nsteps_all / splits);
+
+  int acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0;
+  tile_mainloop<BM, BN, THREADS>(a, m0, n0, k_begin, k_end, acc, sm);
+
+  if (SPLIT) {
+    constexpr int TX = BN / 8;
+    const int tx = threadIdx.x % TX;
+    const int ty = threadIdx.x / TX;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int co = m0 + h * (BM / 2) + ty * 4;
+      if (co >= a.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t p = n0 + (j < 4 ? tx * 4 + j : BN / 2 + tx * 4 + (j - 4));
+        if (p >= a.P) continue;
+        int* dst = a.ws + p * a.Cout + co;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (co + i < a.Cout) atomicAdd(dst + i, acc[h * 4 + i][j]);
+      }
+    }
+    return;
+  }
+  tile_epilogue<BM, BN, THREADS, OUT_NHWC>(a, m0, n0, acc);
+}
+
+// Stream-K schedule (NHWC outputs): exactly one resident round of G blocks; the tiles x
+// K-steps work units are divided evenly, block b taking units [b*U/G, (b+1)*U/G) in tile
+// order.  Whole tiles get the epilogue at once; the (at most two) partial tiles at the ends
+// of a block's range park their int32 partial sums in the block's two slabs with plain
+// 16-byte stores, and conv2d_tp_streamk_fixup sums a tile's slabs and runs its epilogue.
+// No atomics, no inter-block synchronisation inside a launch.
+__device__ __forceinline__ int64_t sk_bound(int64_t b, int64_t U, int64_t G) {
+  return b * U / G;
+}
+
+template <int BM, int BN, int THREADS>
+__device__ __forceinline__ int32_t* sk_slab(const ConvArgs& a, int64_t b, int slot) {
+  return a.ws + (b * 2 + slot) * (int64_t)(BM * BN);
+}
+
+template <int BM, int BN, int THREADS, int OCC>
+__global__ __launch_bounds__(THREADS, OCC) void conv2d_tp_streamk_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) TileSmem<BM, BN> sm;
+  const int64_t G = gridDim.x;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int64_t tiles = ((a.P + BN - 1) / BN) * mt;
+  const int nsteps = a.Kp / 32;
+  const int64_t U = tiles * nsteps;
+  const int64_t u0 = sk_bound(b, U, G), u1 = sk_bound(b + 1, U, G);
+  int64_t u = u0;
+  while (u < u1) {
+    const int64_t t = u / nsteps;
+    const int k0 = (int)(u - t * nsteps);
+    const int k1 = (int)min((int64_t)nsteps, (int64_t)k0 + (u1 - u));
+    const int m0 = (int)(t % mt) * BM;
+    const int64_t n0 = (t / mt) * BN;
+    int acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = 0;
+    tile_mainloop<BM, BN, THREADS>(a, m0, n0, k0, k1, acc, sm);
+    if (k0 == 0 && k1 == nsteps) {
+      tile_epilogue<BM, BN, THREADS, true>(a, m0, n0, acc);
+    } else {
+      int4* slab = reinterpret_cast<int4*>(sk_slab<BM, BN, THREADS>(a, b, u == u0 ? 0 : 1));
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        slab[q * THREADS + threadIdx.x] =
+            make_int4(acc[q >> 1][(q & 1) * 4 + 0], acc[q >> 1][(q & 1) * 4 + 1],
+                      acc[q >> 1][(q & 1) * 4 + 2], acc[q >> 1][(q & 1) * 4 + 3]);
+    }
+    u += k1 - k0;
+  }
+}
+
+// One block per inner boundary b (1..G-1): if the boundary splits a tile and is the first
+// boundary inside it, sum that tile's slabs from every block whose range touches it (a
+// tile is slot 0 of a block iff it is the block's first tile) and apply the epilogue.
+template <int BM, int BN, int THREADS>
+__global__ __launch_bounds__(THREADS) void conv2d_tp_streamk_fixup(ConvArgs a, int G) {
+  const int64_t b = (int64_t)blockIdx.x + 1;
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int64_t tiles = ((a.P + BN - 1) / BN) * mt;
+  const int nsteps = a.Kp / 32;
+  const int64_t U = tiles * nsteps;
+  const int64_t ub = sk_bound(b, U, G);
+  if (ub % nsteps == 0 || ub >= U) return;           // boundary on a tile edge
+  const int64_t t = ub / nsteps;
+  if (sk_bound(b - 1, U, G) > t * nsteps) return;     // not the first boundary in tile t
+  int acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0;
+  for (int64_t bb = b - 1; bb < G && sk_bound(bb, U, G) < (t + 1) * nsteps; ++bb) {
+    if (sk_bound(bb + 1, U, G) <= t * nsteps) continue;  // empty range before the tile
+    const int slot = (sk_bound(bb, U, G) / nsteps == t) ? 0 : 1;
+    const int4* slab = reinterpret_cast<const int4*>(sk_slab<BM, BN, THREADS>(a, bb, slot));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int4 s = slab[q * THREADS + threadIdx.x];
+      acc[q >> 1][(q & 1) * 4 + 0] += s.x;
+      acc[q >> 1][(q & 1) * 4 + 1] += s.y;
+      acc[q >> 1][(q & 1) * 4 + 2] += s.z;
+      acc[q >> 1][(q & 1) * 4 + 3] += s.w;
+    }
+  }
+  const int m0 = (int)(t % mt) * BM;
+  const int64_t n0 = (t / mt) * BN;
+  tile_epilogue<BM, BN, THREADS, true>(a, m0, n0, acc);
 }
 
 // Split-K epilogue: 4 channels of one pixel per lane from the int32 workspace.
@@ -397,13 +510,13 @@ hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, 
   return hipGetLastError();
 }
 
-// Tile configurations: {BM, BN, threads}.  All keep 8 x 8 accumulators per lane.
+// Tile configurations: {BM, BN, threads, waves per SIMD}.  All keep 8 x 8 accumulators per
+// lane; configs 4 and 5 repeat 0 and 1 with a 4-waves-per-SIMD register budget.
 struct TileCfg {
-  int bm, bn, threads;
+  int bm, bn, threads, occ;
 };
-constexpr TileCfg kTileCfgs[] = {{128, 128, 256}, {64, 256, 256}, {64, 128, 128},
-                                 {128, 64, 128},  {128, 128, 256}, {64, 256, 256}};
-// configs 4 and 5 repeat 0 and 1 with a 4-waves-per-SIMD register budget (128 VGPRs)
+constexpr TileCfg kTileCfgs[] = {{128, 128, 256, 3}, {64, 256, 256, 3}, {64, 128, 128, 3},
+                                 {128, 64, 128, 3},  {128, 128, 256, 4}, {64, 256, 256, 4}};
 constexpr int kNumTileCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
 
 int conv_tile_m(int64_t cout) { return cout <= 64 ? 64 : 128; }
@@ -412,31 +525,88 @@ int conv_num_configs() { return kNumTileCfgs; }
 
 namespace {
 
-// Heuristic for config 0, from the per-layer sweep of tools/microbench.py --sweep on MI355X
-// (profiles/r01_sweep.txt): 64x256 tiles for Cout <= 64, else 128x128, one K pass; only when
-// the 128x128 grid leaves most CUs with < 2 tiles and K is deep (ResNet-18 layer4 3x3) does
-// a 3-way K split of 128x64 tiles pay for its int32 atomics (~12 %).  Splitting any larger
-// grid costs more in atomics than it gains (2-4x slower at layer1).
+int device_cus() {
+  static thread_local int cached_dev = -1, cached_cus = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev != cached_dev) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached_dev = dev;
+    cached_cus = cus;
+  }
+  return cached_cus;
+}
+
+// Resident blocks per CU of the stream-K kernel of one config (occupancy query, cached).
+template <int BM, int BN, int T, int OCC>
+int streamk_blocks_per_cu() {
+  static thread_local int cached = 0;
+  if (cached == 0) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &n, reinterpret_cast<const void*>(&conv2d_tp_streamk_kernel<BM, BN, T, OCC>), T,
+            0) != hipSuccess || n <= 0)
+      n = 1;
+    cached = n;
+  }
+  return cached;
+}
+
+int streamk_grid(int cfg) {
+  int per_cu = 1;
+  switch (cfg) {
+    case 0: per_cu = streamk_blocks_per_cu<128, 128, 256, 3>(); break;
+    case 1: per_cu = streamk_blocks_per_cu<64, 256, 256, 3>(); break;
+    case 2: per_cu = streamk_blocks_per_cu<64, 128, 128, 3>(); break;
+    case 3: per_cu = streamk_blocks_per_cu<128, 64, 128, 3>(); break;
+    case 4: per_cu = streamk_blocks_per_cu<128, 128, 256, 4>(); break;
+    default: per_cu = streamk_blocks_per_cu<64, 256, 256, 4>(); break;
+  }
+  return device_cus() * per_cu;
+}
+
+// Execution plan for config 0 (heuristic), from tools/microbench.py --sweep on MI355X
+// (profiles/r01_sweep2.txt): 64x256 tiles for Cout <= 64, else 128x128.  The dot2 pipe is
+// saturated while 3 waves share a SIMD, so a data-parallel grid whose last round of blocks
+// is partly empty loses that fraction (1568 tiles on 768 slots ran at 68 %); stream-K (one
+// resident round, K-steps shared evenly, slab fixup) recovers it when the grid is under
+// 2.5 rounds and K is deep enough (>= 32 steps) to amortise the fixup -- ResNet-18
+// layer2-4 3x3 convs gain 2-24 %; layer1 and all 1x1 convs stay data-parallel.
+// splits: 1 = data-parallel, > 1 = K-split with atomics, -1 = stream-K.
 void pick_config(const ConvArgs& a, int out_nhwc, int* cfg, int* splits) {
   if (a.config > 0 && a.config <= kNumTileCfgs) {
     *cfg = a.config - 1;
-    *splits = a.splits > 0 ? a.splits : 1;
+    *splits = a.splits != 0 ? a.splits : 1;
   } else {
     *cfg = a.Cout <= 64 ? 1 : 0;
     *splits = 1;
-    const int64_t tiles128 = ((a.P + 127) / 128) * ((a.Cout + 127) / 128);
-    const int nsteps = a.Kp / 32;
-    if (a.Cout > 64 && tiles128 < 2 * 256 && nsteps >= 96) {
-      *cfg = 3;
-      *splits = 3;
-    }
+    const TileCfg& t = kTileCfgs[*cfg];
+    const int64_t tiles = ((a.P + t.bn - 1) / t.bn) * ((a.Cout + t.bm - 1) / t.bm);
+    const int64_t slots = (int64_t)device_cus() * 3;
+    const double rounds = (double)tiles / (double)slots;
+    const double eff = rounds / std::ceil(rounds);
+    if (eff < 0.9 && rounds < 2.5 && a.Kp / 32 >= 32) *splits = -1;
   }
-  if (!out_nhwc || !a.ws || (a.Cout & 3)) *splits = 1;  // split-K only for NHWC outputs
+  if (!out_nhwc || !a.ws || (a.Cout & 3)) *splits = 1;  // both need NHWC + a workspace
 }
 
 template <int BM, int BN, int T, int OCC>
 hipError_t launch_cfg(const ConvArgs& a, int out_nhwc, int splits, hipStream_t stream) {
   const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + BM - 1) / BM);
+  if (splits < 0) {
+    const int64_t units = tiles * (a.Kp / 32);
+    int64_t g = (int64_t)device_cus() * streamk_blocks_per_cu<BM, BN, T, OCC>();
+    if (g > units) g = units;
+    if ((int64_t)g * 2 * BM * BN * 4 > a.ws_bytes) return hipErrorInvalidValue;
+    conv2d_tp_streamk_kernel<BM, BN, T, OCC><<<dim3((unsigned)g), T, 0, stream>>>(a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || g < 2) return e;
+    conv2d_tp_streamk_fixup<BM, BN, T><<<dim3((unsigned)(g - 1)), T, 0, stream>>>(a, (int)g);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)(tiles * splits));
   if (splits > 1)
     conv2d_tp_kernel<BM, BN, T, true, true, OCC><<<grid, T, 0, stream>>>(a);
@@ -449,11 +619,22 @@ hipError_t launch_cfg(const ConvArgs& a, int out_nhwc, int splits, hipStream_t s
 
 }  // namespace
 
+int64_t conv_workspace_bytes(int64_t p, int64_t cout) {
+  int64_t sk = 0;
+  for (int c = 0; c < kNumTileCfgs; ++c) {
+    const int64_t b = (int64_t)streamk_grid(c) * 2 * kTileCfgs[c].bm * kTileCfgs[c].bn * 4;
+    if (b > sk) sk = b;
+  }
+  const int64_t split = p * cout * 4;
+  return sk > split ? sk : split;
+}
+
 hipError_t launch_conv2d_tp(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
   ConvArgs a = a_in;
   int cfg, splits;
   pick_config(a, out_nhwc, &cfg, &splits);
+  if (splits > 1 && a.P * a.Cout * 4 > a.ws_bytes) splits = 1;
   a.splits = splits;
   if (splits > 1) {
     hipError_t e = hipMemsetAsync(a.ws, 0, (size_t)a.P * a.Cout * sizeof(int32_t), stream);
@@ -468,7 +649,7 @@ hipError_t launch_conv2d_tp(const ConvArgs& a_in, int out_nhwc, hipStream_t stre
     case 4: e = launch_cfg<128, 128, 256, 4>(a, out_nhwc, splits, stream); break;
     default: e = launch_cfg<64, 256, 256, 4>(a, out_nhwc, splits, stream); break;
   }
-  if (e != hipSuccess || splits == 1) return e;
+  if (e != hipSuccess || splits <= 1) return e;
   const int64_t n = a.P * (a.Cout / 4);
   conv_finalize_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(a);
   return hipGetLastError();

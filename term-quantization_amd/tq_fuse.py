@@ -81,7 +81,7 @@ class _Conv(object):
             res = residual if residual.is_contiguous(memory_format=torch.channels_last) \
                 else residual.contiguous(memory_format=torch.channels_last)
         cin = self.layer.conv.in_channels
-        ws = torch.empty(n * ho * wo * self.cout, dtype=torch.int32, device=dev)
+        ws = tq_native.conv2d_workspace(n * ho * wo, self.cout, dev)
         tq_ops._launch(
             "conv2d_termpair", n * ho * wo * self.cout * cin * self.kh * self.kw,
             lambda: tq_native.conv2d_termpair_fused(

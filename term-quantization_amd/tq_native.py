@@ -37,6 +37,7 @@ _SIGNATURES = {
     "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _vp],
     "tq_conv2d_cout_align": [],
     "tq_conv2d_num_configs": [],
+    "tq_conv2d_workspace_bytes": [_i64, _i64],
     "tq_conv2d_termpair": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64,
                            _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32,
                            _vp],
@@ -52,7 +53,8 @@ class ConvEpilogue(ctypes.Structure):
                 ("terms_a", _i32),
                 ("codes_b", _vp), ("cp_b", _i64), ("sf_b", _f32), ("bits_b", _i32),
                 ("terms_b", _i32),
-                ("workspace", _vp), ("split_k", _i32), ("config", _i32)]
+                ("workspace", _vp), ("workspace_bytes", _i64), ("split_k", _i32),
+                ("config", _i32)]
 
 
 _SIGNATURES["tq_conv2d_termpair_fused"] = [
@@ -60,7 +62,8 @@ _SIGNATURES["tq_conv2d_termpair_fused"] = [
     _i64, _f64, _vp, _vp, _i64, _i64, ctypes.POINTER(ConvEpilogue), _vp]
 
 _RESTYPE = {"tq_version": ctypes.c_char_p, "tq_last_error": ctypes.c_char_p,
-            "tq_conv2d_cout_align": _i64, "tq_conv2d_num_configs": _i32}
+            "tq_conv2d_cout_align": _i64, "tq_conv2d_num_configs": _i32,
+            "tq_conv2d_workspace_bytes": _i64}
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 
@@ -178,6 +181,8 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
         epi.codes_b, epi.cp_b = _ptr(codes_b), codes_b.shape[-1]
         epi.sf_b, epi.bits_b, epi.terms_b = float(quant_b[0]), int(quant_b[1]), int(quant_b[2])
     epi.workspace, epi.split_k, epi.config = _ptr(workspace), int(split_k), int(config)
+    epi.workspace_bytes = workspace.numel() * workspace.element_size() if workspace is not None \
+        else 0
     with torch.cuda.device(codes.device):
         rc = lib().tq_conv2d_termpair_fused(
             _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1], stride[0],
@@ -198,3 +203,10 @@ def dwconv2d_termpair(codes, c, w_codes, kh, kw, stride, pad_tl, dilation, scale
                                         _ptr(out), ho, wo, int(out_nhwc), _stream(codes))
     _check(rc)
     return out
+
+
+def conv2d_workspace(pixels, cout, device):
+    """Scratch for the K-split schedules of tq_conv2d_termpair_fused (int32 tensor)."""
+    with torch.cuda.device(device):
+        nbytes = int(lib().tq_conv2d_workspace_bytes(int(pixels), int(cout)))
+    return torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=device)

@@ -16,6 +16,15 @@ for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
         sys.path.insert(0, p)
 
 
+# (cin, cout, k, stride, hin) of the 19 ResNet-18 TR convs
+RESNET18_TR = [(64, 64, 3, 1, 56)] * 4 + [(64, 128, 3, 2, 56), (128, 128, 3, 1, 28),
+                                          (64, 128, 1, 2, 56)] + \
+    [(128, 128, 3, 1, 28)] * 2 + [(128, 256, 3, 2, 28), (256, 256, 3, 1, 14),
+                                  (128, 256, 1, 2, 28)] + \
+    [(256, 256, 3, 1, 14)] * 2 + [(256, 512, 3, 2, 14), (512, 512, 3, 1, 7),
+                                  (256, 512, 1, 2, 14)] + [(512, 512, 3, 1, 7)] * 2
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 

@@ -85,3 +85,44 @@ def test_fused_resnet_matches_module_path():
     rel = (got - ref).norm() / ref.norm()
     assert rel.item() < 1e-3, rel.item()
     assert (got.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.75
+
+
+@pytest.mark.parametrize("layer,cfgs", [(1, [(2, 1), (2, -1), (6, -1)]),
+                                         (6, [(1, 1), (1, -1), (5, -1), (4, -1)]),
+                                         (16, [(1, 1), (1, -1), (4, -1), (4, 3)]),
+                                         (17, [(1, 1), (1, -1), (3, -1)])])
+def test_schedules_are_bit_identical(layer, cfgs):
+    """Data-parallel, K-split (atomics) and stream-K (slab fixup) schedules sum the same
+    integers, so every output and code must be bit-identical."""
+    import tq_ops
+    from conftest import RESNET18_TR
+    cin, cout, k, s, hin = RESNET18_TR[layer - 1]
+    batch = 37  # odd pixel count: partial last tile
+    torch.manual_seed(layer)
+    conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(DEV)
+    lay = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    cp = tq_ops.act_channels(cin)
+    x = torch.relu(torch.randn(batch, cin, hin, hin, device=DEV)).to(
+        memory_format=torch.channels_last)
+    codes = torch.empty((batch, hin, hin, cp), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    ho = (hin + 2 * (k // 2) - k) // s + 1
+    ws = tq_native.conv2d_workspace(batch * ho * ho, cout, DEV)
+    sc = torch.rand(cout, dtype=torch.float64, device=DEV) * 1e-4
+    sh = torch.randn(cout, dtype=torch.float64, device=DEV)
+    outs = []
+    for cfg, sp in cfgs:
+        o = torch.full((batch, cout, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.zeros((batch, ho, ho, tq_ops.act_channels(cout)), dtype=torch.int16,
+                         device=DEV)
+        tq_native.conv2d_termpair_fused(codes, lay.w_codes, cout, k, k, (s, s),
+                                        (k // 2, k // 2), (1, 1), ho, ho, out=o, ch_scale=sc,
+                                        ch_shift=sh, relu=True, codes_a=ca,
+                                        quant_a=(0.05, 9, 3), workspace=ws, split_k=sp,
+                                        config=cfg)
+        outs.append((o.cpu(), ca.cpu()))
+    o0, c0 = outs[0]
+    assert not torch.isnan(o0).any()
+    for o, c in outs[1:]:
+        assert torch.equal(o, o0) and torch.equal(c, c0)

@@ -38,7 +38,7 @@ def main():
     tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
     ho = (hin + 2 * (k // 2) - k) // s + 1
     o = torch.empty((args.batch, cout, ho, ho), device=dev, memory_format=torch.channels_last)
-    ws = torch.empty(args.batch * ho * ho * cout, dtype=torch.int32, device=dev)
+    ws = tq_native.conv2d_workspace(args.batch * ho * ho, cout, dev)
     sc = torch.full((cout,), 1e-4, dtype=torch.float64, device=dev)
     sh = torch.zeros(cout, dtype=torch.float64, device=dev)
     fn = lambda: tq_native.conv2d_termpair_fused(
