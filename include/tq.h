@@ -170,6 +170,20 @@ int tq_dwconv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t
                          float *out, int64_t ho, int64_t wo, int32_t out_nhwc, void *stream);
 
 /*
+ * Stem tail of a TQ ResNet in one pass (the stem conv itself stays fp32, as in the
+ * reference): out = relu(maxpool_{k,s,pad}(x * scale[c] + shift[c])) with an eval-mode
+ * BatchNorm as (scale, shift), plus the consuming TR layers' activation codes
+ * codes_a/_b = TR(out; sf, bits, terms) (int16, [n][ho][wo][cp], NULL to skip).
+ * x, out: fp32 channels_last [n][h][w][c] / [n][ho][wo][c], c % 8 == 0, 16-byte aligned.
+ */
+int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, int64_t c,
+                              const float *scale, const float *shift, int32_t k,
+                              int32_t stride, int32_t pad, float *out, int64_t ho, int64_t wo,
+                              int16_t *codes_a, int64_t cp_a, float sf_a, int32_t bits_a,
+                              int32_t terms_a, int16_t *codes_b, int64_t cp_b, float sf_b,
+                              int32_t bits_b, int32_t terms_b, void *stream);
+
+/*
  * Batched activation-scale calibration, replacing the 2048-launch loop of
  * tr_layer.mse_profile (tr_layer.py:43-54):
  *   errs[s] = sum_b hist[b] * (x[b] - TR(x[b]; sf = sfs[s], bitwidth, group 1, k))^2

@@ -298,6 +298,53 @@ int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t
   return hip_status(tq::launch_dwconv_tp(a, (hipStream_t)stream), "dwconv2d launch");
 }
 
+int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, int64_t c,
+                              const float* scale, const float* shift, int32_t k,
+                              int32_t stride, int32_t pad, float* out, int64_t ho, int64_t wo,
+                              int16_t* codes_a, int64_t cp_a, float sf_a, int32_t bits_a,
+                              int32_t terms_a, int16_t* codes_b, int64_t cp_b, float sf_b,
+                              int32_t bits_b, int32_t terms_b, void* stream) {
+  if (n < 0 || h < 1 || w < 1 || c < 8 || c % 8 != 0 || ho < 1 || wo < 1 || k < 1 ||
+      stride < 1 || pad < 0 || pad >= k)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: bad shape or pooling window");
+  if ((ho - 1) * stride - pad >= h || (wo - 1) * stride - pad >= w)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: output larger than the input");
+  if (!x || !out || !scale || !shift || (uintptr_t)x % 16 || (uintptr_t)out % 16)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: null or misaligned buffer");
+  int rc = code_target(codes_a, cp_a, sf_a, bits_a, terms_a, c, "a");
+  if (rc != TQ_OK) return rc;
+  rc = code_target(codes_b, cp_b, sf_b, bits_b, terms_b, c, "b");
+  if (rc != TQ_OK) return rc;
+  if ((codes_a && (uintptr_t)codes_a % 16) || (codes_b && (uintptr_t)codes_b % 16))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: codes must be 16-byte aligned");
+  tq::PoolArgs a;
+  a.x = x;
+  a.scale = scale;
+  a.shift = shift;
+  a.out = out;
+  a.N = (int)n;
+  a.H = (int)h;
+  a.W = (int)w;
+  a.C = (int)c;
+  a.Ho = (int)ho;
+  a.Wo = (int)wo;
+  a.k = k;
+  a.s = stride;
+  a.pad = pad;
+  a.codes_a = codes_a;
+  a.cp_a = (int)cp_a;
+  a.sf_a = sf_a;
+  a.maxv_a = (float)((1u << (codes_a ? bits_a : 0)) - 1u);
+  a.k_a = terms_a < 0 ? 0 : terms_a;
+  a.codes_b = codes_b;
+  a.cp_b = (int)cp_b;
+  a.sf_b = sf_b;
+  a.maxv_b = (float)((1u << (codes_b ? bits_b : 0)) - 1u);
+  a.k_b = terms_b < 0 ? 0 : terms_b;
+  return hip_status(tq::launch_bn_relu_maxpool_encode(a, (hipStream_t)stream),
+                    "bn_relu_maxpool launch");
+}
+
 int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                    int64_t nsf, int32_t bitwidth, int32_t num_keep_terms, double* errs,
                    void* stream) {

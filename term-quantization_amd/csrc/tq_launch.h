@@ -54,6 +54,22 @@ struct DwConvArgs {
 
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream);
 
+struct PoolArgs {
+  const float* x;        // [N][H][W][C] fp32 (channels_last), C % 8 == 0
+  const float* scale;    // [C] BN scale (gamma / sqrt(var + eps))
+  const float* shift;    // [C] BN shift (beta - mean * scale)
+  float* out;            // [N][Ho][Wo][C]
+  int N, H, W, C, Ho, Wo, k, s, pad;
+  int16_t* codes_a;      // [N][Ho][Wo][cp_a] or nullptr
+  int cp_a, k_a;
+  float sf_a, maxv_a;
+  int16_t* codes_b;
+  int cp_b, k_b;
+  float sf_b, maxv_b;
+};
+
+hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
+
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
                              int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,
                              hipStream_t stream);

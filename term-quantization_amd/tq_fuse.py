@@ -102,6 +102,13 @@ class _Block(object):
             self.down = _Conv(block.downsample[0], block.downsample[1])
 
 
+def _pool_params(mp):
+    k, s, p = mp.kernel_size, mp.stride, mp.padding
+    if any(isinstance(v, tuple) for v in (k, s, p)) or mp.dilation != 1 or mp.ceil_mode:
+        return None
+    return int(k), int(s), int(p)
+
+
 class FusedResNet(nn.Module):
     """Inference executor over a converted + calibrated torchvision-style ResNet."""
 
@@ -112,25 +119,55 @@ class FusedResNet(nn.Module):
         for layer in (qmodel.layer1, qmodel.layer2, qmodel.layer3, qmodel.layer4):
             for block in layer:
                 self.blocks.append(_Block(block))
+        # stem tail: eval BN as an fp32 per-channel affine for the fused pool+encode pass
+        bn = qmodel.bn1
+        self.pool = _pool_params(qmodel.maxpool)
+        a = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+        self.stem_scale = a.float().contiguous()
+        self.stem_shift = (bn.bias.detach().double() -
+                           bn.running_mean.detach().double() * a).float().contiguous()
+        self.fuse_stem = (self.pool is not None and not bn.training and
+                          bn.num_features % 8 == 0)
+
+    def _stem(self, x):
+        m = self.qmodel
+        first = self.blocks[0]
+        if not self.fuse_stem:
+            x = m.maxpool(m.relu(m.bn1(m.conv1(x)))).contiguous(
+                memory_format=torch.channels_last)
+            codes = torch.empty((x.shape[0], x.shape[2], x.shape[3], first.conv1.cp_in),
+                                dtype=torch.int16, device=x.device)
+            tq_ops._launch("act_encode", 4 * x.numel() + 2 * codes.numel(),
+                           lambda: tq_native.act_encode(x, True, *first.conv1.quant, codes))
+            codes_down = None
+            if first.down is not None:
+                codes_down = torch.empty_like(codes)
+                tq_native.act_encode(x, True, *first.down.quant, codes_down)
+            return x, codes, codes_down
+        y = m.conv1(x).contiguous(memory_format=torch.channels_last)
+        n, c, h, w = y.shape
+        k, s, p = self.pool
+        ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+        out = torch.empty((n, c, ho, wo), dtype=torch.float32, device=y.device,
+                          memory_format=torch.channels_last)
+        codes = torch.empty((n, ho, wo, first.conv1.cp_in), dtype=torch.int16, device=y.device)
+        codes_down = None
+        if first.down is not None:
+            codes_down = torch.empty((n, ho, wo, first.down.cp_in), dtype=torch.int16,
+                                     device=y.device)
+        tq_ops._launch(
+            "stem_pool_encode", 4 * y.numel() + 4 * out.numel() + 2 * codes.numel(),
+            lambda: tq_native.bn_relu_maxpool_encode(
+                y, self.stem_scale, self.stem_shift, k, s, p, out, codes_a=codes,
+                quant_a=first.conv1.quant, codes_b=codes_down,
+                quant_b=first.down.quant if first.down is not None else None))
+        return out, codes, codes_down
 
     @torch.no_grad()
     def forward(self, x):
         m = self.qmodel
         x = x.contiguous(memory_format=torch.channels_last)
-        x = m.maxpool(m.relu(m.bn1(m.conv1(x))))
-        x = x.contiguous(memory_format=torch.channels_last)
-        first = self.blocks[0]
-        codes = torch.empty((x.shape[0], x.shape[2], x.shape[3], first.conv1.cp_in),
-                            dtype=torch.int16, device=x.device)
-        n, c, h, w = x.shape
-        tq_ops._launch("act_encode", 4 * x.numel() + 2 * codes.numel(),
-                       lambda: tq_native.act_encode(x, True, first.conv1.quant[0],
-                                                    first.conv1.quant[1], first.conv1.quant[2],
-                                                    codes))
-        codes_down = None
-        if first.down is not None:
-            codes_down = torch.empty_like(codes)
-            tq_native.act_encode(x, True, *first.down.quant, codes_down)
+        x, codes, codes_down = self._stem(x)
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             _, mid, _ = b.conv1(codes, relu=True, next_a=b.conv2)

@@ -42,6 +42,9 @@ _SIGNATURES = {
                            _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32,
                            _vp],
     "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
+    "tq_bn_relu_maxpool_encode": [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _i32, _i32,
+                                  _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _vp, _i64,
+                                  _f32, _i32, _i32, _vp],
     "tq_dwconv2d_termpair": [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                              _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32, _vp],
 }
@@ -210,3 +213,21 @@ def conv2d_workspace(pixels, cout, device):
     with torch.cuda.device(device):
         nbytes = int(lib().tq_conv2d_workspace_bytes(int(pixels), int(cout)))
     return torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=device)
+
+
+def bn_relu_maxpool_encode(x, scale, shift, k, stride, pad, out, codes_a=None, quant_a=None,
+                           codes_b=None, quant_b=None):
+    """relu(maxpool(bn(x))) into ``out`` plus next layers' codes (channels_last fp32)."""
+    n, c, h, w = x.shape
+    ho, wo = out.shape[2], out.shape[3]
+    qa = quant_a or (0.0, 0, 0)
+    qb = quant_b or (0.0, 0, 0)
+    with torch.cuda.device(x.device):
+        rc = lib().tq_bn_relu_maxpool_encode(
+            _ptr(x), n, h, w, c, _ptr(scale), _ptr(shift), k, stride, pad, _ptr(out), ho, wo,
+            _ptr(codes_a), codes_a.shape[-1] if codes_a is not None else 0, float(qa[0]),
+            int(qa[1]), int(qa[2]), _ptr(codes_b),
+            codes_b.shape[-1] if codes_b is not None else 0, float(qb[0]), int(qb[1]),
+            int(qb[2]), _stream(x))
+    _check(rc)
+    return out

@@ -126,3 +126,26 @@ def test_schedules_are_bit_identical(layer, cfgs):
     assert not torch.isnan(o0).any()
     for o, c in outs[1:]:
         assert torch.equal(o, o0) and torch.equal(c, c0)
+
+
+def test_stem_bn_relu_maxpool_encode():
+    torch.manual_seed(11)
+    bn = nn.BatchNorm2d(64).to(DEV).eval()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.5, 1.5)  # negative scales too: BN before the max
+        bn.bias.uniform_(-0.3, 0.3)
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    x = torch.randn(3, 64, 29, 30, device=DEV).contiguous(memory_format=torch.channels_last)
+    ref = F.max_pool2d(torch.relu(bn(x)), 3, 2, 1)
+    a = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    sc = a.float().contiguous()
+    sh = (bn.bias.double() - bn.running_mean.double() * a).float().contiguous()
+    out = torch.empty_like(ref, memory_format=torch.channels_last)
+    codes = torch.empty((3, ref.shape[2], ref.shape[3], 64), dtype=torch.int16, device=DEV)
+    tq_native.bn_relu_maxpool_encode(x, sc, sh, 3, 2, 1, out, codes_a=codes,
+                                     quant_a=(0.05, 9, 3))
+    assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)
+    yq = oracle.tr(out.contiguous().cpu().numpy().reshape(1, -1, 1, 1), 0.05, 9, 1, 3)
+    exp = np.rint(yq.reshape(out.shape) / np.float32(0.05)).astype(np.int64)
+    assert torch.equal(codes.cpu().long().permute(0, 3, 1, 2), torch.from_numpy(exp))

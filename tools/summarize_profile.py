@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {
     "conv2d_tp": "conv2d_tp_kernel",
     "act_encode": "act_encode_kernel",
+    "stem_pool_encode": "bn_relu_maxpool_encode_kernel",
     "tr_elem": "tr_elem_kernel",
     "tr_group": "tr_group_kernel",
 }
@@ -67,10 +68,12 @@ def main(tag):
         json.dump(summary, fp, indent=1)
     conv = summary["kernels"].get("conv2d_tp", {})
     enc = summary["kernels"].get("act_encode", {})
+    stem = summary["kernels"].get("stem_pool_encode", {})
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as fp:
         json.dump({"source": "profiles/%s_summary.json" % tag,
                    "conv2d_tp_bytes_per_launch": conv.get("hbm_bytes_per_launch"),
-                   "act_encode_bytes_per_launch": enc.get("hbm_bytes_per_launch")}, fp,
+                   "act_encode_bytes_per_launch": enc.get("hbm_bytes_per_launch"),
+                   "stem_pool_encode_bytes_per_launch": stem.get("hbm_bytes_per_launch")}, fp,
                   indent=1)
     for k, v in summary["kernels"].items():
         print(k, {a: b for a, b in v.items() if a != "variants"})
