@@ -38,6 +38,9 @@ VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes x clock = 78.6e12 l
 # v_dot2c_i32_i16 issues at half the VALU rate on gfx950 (4 cycles per wave64; measured
 # 35.8e12 lane-op/s by tools/valu_peak.hip) and does 2 int16 MACs per lane-op:
 DOT2_PEAK = 2 * VALU_LANE_OPS / 2   # 78.6e12 term-sum MAC/s
+# v_mfma_f32_32x32x16_f16: dense fp16 MFMA peak (MI355X_MICROARCH.md, matrix cores; the
+# 2:1-sparsity headline is not a dense rate) -- 2 FLOP per term-sum product
+MFMA_F16_PEAK_TFLOPS = 2500.0
 
 
 def parse():
@@ -49,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=24,
                     help="images in the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--engine", choices=("mfma", "valu"), default="mfma",
+                    help="term-pair engine: MFMA (fp16 codes) or VALU (int16 codes, "
+                         "v_dot2c_i32_i16); bit-identical outputs")
     ap.add_argument("--unfused", action="store_true",
                     help="run the module path (separate BN/ReLU/add/TR passes) instead of "
                          "the fused executor")
@@ -88,6 +94,8 @@ def build_model(dev, batch, seed):
     qmodel = cnn_models.convert_model(model, settings, DB, DT)
     qmodel = qmodel.to(memory_format=torch.channels_last)
     assert all(m.termpair for m in qmodel.modules() if isinstance(m, tr_layer.TRConv2dLayer))
+    engines = {m.engine for m in qmodel.modules() if isinstance(m, tr_layer.TRConv2dLayer)}
+    assert engines == {os.environ["TQ_CONV_ENGINE"]}, engines
     # term-pair MACs per image (profile_model, 1x3x224x224 -- evaluate_cnn.py:28-29)
     tmacs, _ = profile_model.get_model_ops(qmodel, (torch.randn(1, 3, 224, 224, device=dev),))
     # calibration: one tracking pass on this rank's calibration batch, histograms summed
@@ -150,6 +158,7 @@ def cpu_baseline(model_fp, qmodel, nimg):
 
 def main():
     args = parse()
+    os.environ["TQ_CONV_ENGINE"] = args.engine
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -216,11 +225,39 @@ def main():
         enc_t = enc["seconds"] / enc["launches"]
         enc_bytes = enc["work"] / enc["launches"]
         traffic = enc_traffic = None
+        mfma = args.engine == "mfma"
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
             pmc = json.load(open(pmc_path))
-            traffic = pmc.get("conv2d_tp_bytes_per_launch")
+            traffic = pmc.get("conv2d_tp_mfma_bytes_per_launch" if mfma else
+                              "conv2d_tp_bytes_per_launch")
             enc_traffic = pmc.get(enc_name + "_bytes_per_launch")
+        if mfma:
+            roof = {
+                "kernel": "conv2d_tp_mfma_kernel (term-pair conv, exact fp16 term sums, "
+                          "v_mfma_f32_32x32x16_f16, int32 sums)",
+                "bound": "mfma",
+                "achieved": 2 * conv_work / conv_t / 1e12,
+                "peak": MFMA_F16_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": 2 * conv_work / conv_t / 1e12 / MFMA_F16_PEAK_TFLOPS,
+            }
+        else:
+            roof = {
+                "kernel": "conv2d_tp_kernel (term-pair conv, int16 term sums, v_dot2c_i32_i16)",
+                "bound": "valu",
+                "achieved": conv_work / conv_t / 1e12,
+                "peak": DOT2_PEAK / 1e12,
+                "unit": "TMAC/s (int16 term-sum products)",
+                "frac": conv_work / conv_t / DOT2_PEAK,
+            }
+        roof.update({
+            "traffic": traffic,
+            "algorithmic_macs_per_launch": conv_work,
+            "avg_launch_us": conv_t * 1e6,
+            "launches": conv["launches"],
+            "share_of_step": conv["seconds"] / elapsed,
+        })
         result = {
             "metric": METRIC,
             "value": ips,
@@ -232,34 +269,23 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int16",
+            "dtype": "f16" if mfma else "int16",
             "data": "synthetic",
             "config": {"workload": "resnet18-tq-g8-k12 (wb=db=9, dt=3), synthetic N(0,1) "
                                    "3x224x224, random-init weights",
                        "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                        "parallelism": "dp%d (batch-sharded, no data-path collective)" % world,
+                       "engine": args.engine,
                        "executor": "module path" if args.unfused else
                                    "fused (BN/ReLU/residual/next-layer TR in the conv "
                                    "epilogue)"},
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,
-            "roofline": {
-                "kernel": "conv2d_tp_kernel (term-pair conv, int16 term sums, v_dot2c_i32_i16)",
-                "bound": "valu",
-                "achieved": conv_work / conv_t / 1e12,
-                "peak": DOT2_PEAK / 1e12,
-                "unit": "TMAC/s (int16 term-sum products)",
-                "frac": conv_work / conv_t / DOT2_PEAK,
-                "traffic": traffic,
-                "algorithmic_macs_per_launch": conv_work,
-                "avg_launch_us": conv_t * 1e6,
-                "launches": conv["launches"],
-                "share_of_step": conv["seconds"] / elapsed,
-            },
+            "roofline": roof,
             "roofline_tr": {
                 "kernel": ("bn_relu_maxpool_encode_kernel (stem BN/ReLU/max-pool + activation "
-                           "TR -> int16 codes)" if enc_name == "stem_pool_encode" else
-                           "act_encode_kernel (TR of activations -> int16 codes)"),
+                           "TR -> 16-bit codes)" if enc_name == "stem_pool_encode" else
+                           "act_encode_kernel (TR of activations -> 16-bit codes)"),
                 "bound": "hbm",
                 "achieved": enc_bytes / enc_t / 1e9,
                 "peak": HBM_PEAK_GBS,

@@ -28,6 +28,13 @@ enum {
   TQ_ERR_HIP = 3               /* a HIP runtime error (launch or memset) */
 };
 
+/*
+ * Code formats of the term-pair kernels: the signed integer term sum v of an element,
+ * stored in 16 bits either as int16 (VALU engine, bitwidth <= 14) or as the fp16 number v
+ * (MFMA engine, exact for bitwidth <= 11).
+ */
+enum { TQ_CODES_I16 = 0, TQ_CODES_F16 = 1 };
+
 /* Library version string, e.g. "tq-hip 0.1.0 gfx950". */
 const char *tq_version(void);
 
@@ -65,13 +72,14 @@ int tq_tr_encode_f32(const float *input, float *output, int32_t *codes, int64_t 
                      int32_t num_keep_terms, void *stream);
 
 /*
- * Activation TR (group_size 1, tr_layer.py:96-99) from fp32 straight into int16 term-sum
+ * Activation TR (group_size 1, tr_layer.py:96-99) from fp32 straight into 16-bit term-sum
  * codes in NHWC with `cp` channels per pixel (cp % 8 == 0, cp >= c, pad channels = 0).
- * `in_nhwc` = 1 for a channels_last input, 0 for NCHW.  Domain: 0 <= bitwidth <= 14.
+ * `in_nhwc` = 1 for a channels_last input, 0 for NCHW.  `fmt` = TQ_CODES_I16 (bitwidth
+ * <= 14) or TQ_CODES_F16 (bitwidth <= 11).
  */
 int tq_act_encode(const float *x, int32_t in_nhwc, int64_t n, int64_t c, int64_t h, int64_t w,
-                  float sf, int32_t bitwidth, int32_t num_keep_terms, int16_t *codes,
-                  int64_t cp, void *stream);
+                  float sf, int32_t bitwidth, int32_t num_keep_terms, void *codes,
+                  int64_t cp, int32_t fmt, void *stream);
 
 /* Rows the weight-code matrix of tq_conv2d_termpair must be padded to (a multiple of). */
 int64_t tq_conv2d_cout_align(void);
@@ -105,8 +113,8 @@ int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w
  *   y = y + residual[p][c]            (fp32, if residual; [P][cout] channels_last)
  *   y = max(y, 0)                     (if relu)
  *   out[p][c] = y                     (if out)
- *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   int16, [P][cp_a] (if codes_a)
- *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   int16, [P][cp_b] (if codes_b)
+ *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   format fmt_a, [P][cp_a] (if codes_a)
+ *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   format fmt_b, [P][cp_b] (if codes_b)
  * codes_a/_b are the next TR layers' activation codes (tr_layer.py:96-99 applied to y), so
  * those layers skip their own activation pass.  cp_* = roundup(cout, 8); cout % 4 == 0.
  */
@@ -135,6 +143,9 @@ typedef struct tq_conv_epilogue {
   int64_t workspace_bytes;
   int32_t split_k;
   int32_t config;
+  /* code formats (TQ_CODES_*) of codes_a / codes_b: the format of the consuming kernel */
+  int32_t fmt_a;
+  int32_t fmt_b;
 } tq_conv_epilogue;
 
 /* Scratch bytes that let tq_conv2d_termpair_fused use any K-split schedule for an output of
@@ -150,6 +161,30 @@ int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int
                              int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
                              double scale, const float *bias, float *out, int64_t ho,
                              int64_t wo, const tq_conv_epilogue *epi, void *stream);
+
+/*
+ * Term-pair Conv2d (groups = 1) on the matrix cores: the same exact integer sums as
+ * tq_conv2d_termpair(_fused), from fp16 codes (TQ_CODES_F16) with v_mfma_f32_32x32x16_f16.
+ * fp32 accumulators are exact while every partial sum stays below 2^24; the caller passes
+ * `kc_steps` >= 1 such that for every weight row m and every window of kc_steps K-steps of
+ * 64 codes, max|act_code| * sum_{k in window} |w_codes[m][k]| < 2^24 (0 = the whole K
+ * range satisfies it), and max_m sum_k |w_codes[m][k]| * max|act_code| < 2^31.
+ *   act_codes  [n][h][w][cp] fp16 codes, 16-byte aligned
+ *   w_codes    [cout_pad][kp] fp16 codes, cout_pad a multiple of tq_conv2d_cout_align(),
+ *              kp a multiple of 64
+ * epi == NULL: out = fp32(acc * scale) + bias, NCHW (out_nhwc = 0) or NHWC (out_nhwc = 1).
+ * epi != NULL: the fused epilogue of tq_conv2d_termpair_fused (out_nhwc must be 1; its
+ * split_k must be 0 or 1: the MFMA engine runs data-parallel tiles).
+ */
+int32_t tq_conv2d_mfma_num_configs(void);
+
+int tq_conv2d_termpair_f16(const uint16_t *act_codes, int64_t n, int64_t h, int64_t w,
+                           int64_t cp, const uint16_t *w_codes, int64_t cout, int64_t kh,
+                           int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
+                           int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                           double scale, const float *bias, float *out, int64_t ho, int64_t wo,
+                           int32_t out_nhwc, int32_t kc_steps, const tq_conv_epilogue *epi,
+                           void *stream);
 
 /*
  * Depthwise term-pair Conv2d (groups == C_in == C_out): per output channel c,
@@ -173,15 +208,16 @@ int tq_dwconv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t
  * Stem tail of a TQ ResNet in one pass (the stem conv itself stays fp32, as in the
  * reference): out = relu(maxpool_{k,s,pad}(x * scale[c] + shift[c])) with an eval-mode
  * BatchNorm as (scale, shift), plus the consuming TR layers' activation codes
- * codes_a/_b = TR(out; sf, bits, terms) (int16, [n][ho][wo][cp], NULL to skip).
+ * codes_a/_b = TR(out; sf, bits, terms) ([n][ho][wo][cp] in format fmt_*, NULL to skip).
  * x, out: fp32 channels_last [n][h][w][c] / [n][ho][wo][c], c % 8 == 0, 16-byte aligned.
  */
 int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, int64_t c,
                               const float *scale, const float *shift, int32_t k,
                               int32_t stride, int32_t pad, float *out, int64_t ho, int64_t wo,
-                              int16_t *codes_a, int64_t cp_a, float sf_a, int32_t bits_a,
-                              int32_t terms_a, int16_t *codes_b, int64_t cp_b, float sf_b,
-                              int32_t bits_b, int32_t terms_b, void *stream);
+                              void *codes_a, int64_t cp_a, float sf_a, int32_t bits_a,
+                              int32_t terms_a, int32_t fmt_a, void *codes_b, int64_t cp_b,
+                              float sf_b, int32_t bits_b, int32_t terms_b, int32_t fmt_b,
+                              void *stream);
 
 /*
  * Batched activation-scale calibration, replacing the 2048-launch loop of

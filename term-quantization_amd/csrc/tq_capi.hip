@@ -20,6 +20,9 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// Largest bitwidth whose term sums (|v| <= 2^bitwidth) a code format holds exactly.
+int max_code_bits(int fmt) { return fmt == TQ_CODES_F16 ? 11 : 14; }
+
 int hip_status(hipError_t e, const char* what) {
   if (e == hipSuccess) return TQ_OK;
   return fail(TQ_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
@@ -96,22 +99,25 @@ int tq_tr_encode_f32(const float* input, float* output, int32_t* codes, int64_t 
 }
 
 int tq_act_encode(const float* x, int32_t in_nhwc, int64_t n, int64_t c, int64_t h, int64_t w,
-                  float sf, int32_t bitwidth, int32_t num_keep_terms, int16_t* codes,
-                  int64_t cp, void* stream) {
+                  float sf, int32_t bitwidth, int32_t num_keep_terms, void* codes, int64_t cp,
+                  int32_t fmt, void* stream) {
   if (n < 0 || c < 1 || h < 0 || w < 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: bad shape");
   if (cp < c || cp % 8 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: cp must be >= c and a multiple of 8");
-  if (bitwidth < 0 || bitwidth > 14)
-    return fail(TQ_ERR_UNSUPPORTED, "act_encode: int16 codes need bitwidth <= 14 (got %d)",
-                bitwidth);
+  if (fmt != TQ_CODES_I16 && fmt != TQ_CODES_F16)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: unknown code format %d", fmt);
+  if (bitwidth < 0 || bitwidth > max_code_bits(fmt))
+    return fail(TQ_ERR_UNSUPPORTED, "act_encode: %s codes need bitwidth <= %d (got %d)",
+                fmt == TQ_CODES_F16 ? "fp16" : "int16", max_code_bits(fmt), bitwidth);
   if (!(sf >= 0.0f)) return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: sf must be >= 0");
   if ((uintptr_t)codes % 16 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: codes must be 16-byte aligned");
   if (in_nhwc && cp == c && (uintptr_t)x % 16 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode: x must be 16-byte aligned");
   const int kk = num_keep_terms < 0 ? 0 : num_keep_terms;
-  return hip_status(tq::launch_act_encode(x, in_nhwc, n, c, h, w, sf, bitwidth, kk, codes, cp,
+  return hip_status(tq::launch_act_encode(x, in_nhwc, n, c, h, w, sf, bitwidth, kk,
+                                          static_cast<int16_t*>(codes), cp, fmt,
                                           (hipStream_t)stream),
                     "act_encode launch");
 }
@@ -119,6 +125,8 @@ int tq_act_encode(const float* x, int32_t in_nhwc, int64_t n, int64_t c, int64_t
 int64_t tq_conv2d_cout_align(void) { return 128; }
 
 int32_t tq_conv2d_num_configs(void) { return tq::conv_num_configs(); }
+
+int32_t tq_conv2d_mfma_num_configs(void) { return tq::conv_mfma_num_configs(); }
 
 int64_t tq_conv2d_workspace_bytes(int64_t pixels, int64_t cout) {
   return tq::conv_workspace_bytes(pixels, cout);
@@ -176,16 +184,63 @@ int conv_common(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64
   return TQ_OK;
 }
 
-int code_target(int16_t* codes, int64_t cp, float sf, int32_t bits, int32_t terms,
-                int64_t cout, const char* which) {
+int code_target(const void* codes, int64_t cp, float sf, int32_t bits, int32_t terms,
+                int32_t fmt, int64_t cout, const char* which) {
   if (codes == nullptr) return TQ_OK;
   if (cp < cout || cp % 8 != 0 || (uintptr_t)codes % 8 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d epilogue: codes_%s needs cp >= cout, "
                 "cp %% 8 == 0 and 8-byte alignment", which);
-  if (bits < 0 || bits > 14)
-    return fail(TQ_ERR_UNSUPPORTED, "conv2d epilogue: codes_%s bitwidth must be <= 14", which);
+  if (fmt != TQ_CODES_I16 && fmt != TQ_CODES_F16)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "codes_%s: unknown code format %d", which, fmt);
+  if (bits < 0 || bits > max_code_bits(fmt))
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d epilogue: codes_%s bitwidth must be <= %d", which,
+                max_code_bits(fmt));
   if (!(sf >= 0.0f))
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d epilogue: codes_%s sf must be >= 0", which);
+  return TQ_OK;
+}
+
+// Fill the fused-epilogue fields of `a` from `epi` (shared by both conv engines).
+int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int num_configs,
+                   tq::ConvArgs* a) {
+  if (cout % 4 != 0)
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d fused epilogue needs cout %% 4 == 0");
+  if ((epi->ch_scale == nullptr) != (epi->ch_shift == nullptr))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: ch_scale and ch_shift go together");
+  if (out == nullptr && epi->codes_a == nullptr && epi->codes_b == nullptr)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: no output requested");
+  if ((out && (uintptr_t)out % 16) || (epi->residual && (uintptr_t)epi->residual % 16))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: out/residual must be 16-byte aligned");
+  int rc = code_target(epi->codes_a, epi->cp_a, epi->sf_a, epi->bits_a, epi->terms_a,
+                       epi->fmt_a, cout, "a");
+  if (rc != TQ_OK) return rc;
+  rc = code_target(epi->codes_b, epi->cp_b, epi->sf_b, epi->bits_b, epi->terms_b, epi->fmt_b,
+                   cout, "b");
+  if (rc != TQ_OK) return rc;
+  a->ch_scale = epi->ch_scale;
+  a->ch_shift = epi->ch_shift;
+  a->residual = epi->residual;
+  a->relu = epi->relu;
+  a->codes_a = epi->codes_a;
+  a->cp_a = (int)epi->cp_a;
+  a->sf_a = epi->sf_a;
+  a->maxv_a = (float)((1u << (epi->codes_a ? epi->bits_a : 0)) - 1u);
+  a->k_a = epi->terms_a < 0 ? 0 : epi->terms_a;
+  a->fmt_a = epi->fmt_a;
+  a->codes_b = epi->codes_b;
+  a->cp_b = (int)epi->cp_b;
+  a->sf_b = epi->sf_b;
+  a->maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
+  a->k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
+  a->fmt_b = epi->fmt_b;
+  if (epi->config < 0 || epi->config > num_configs || epi->split_k < -1 || epi->split_k > 64)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
+  if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: workspace must be 16-byte aligned");
+  a->config = epi->config;
+  a->splits = epi->split_k;
+  a->ws = epi->workspace;
+  a->ws_bytes = epi->workspace ? epi->workspace_bytes : 0;
   return TQ_OK;
 }
 
@@ -217,42 +272,39 @@ int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int
                        pad_h, pad_w, dil_h, dil_w, scale, bias, out, ho, wo, &a);
   if (rc != TQ_OK) return rc;
   if (epi == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: epilogue is null");
-  if (cout % 4 != 0)
-    return fail(TQ_ERR_UNSUPPORTED, "conv2d fused epilogue needs cout %% 4 == 0");
-  if ((epi->ch_scale == nullptr) != (epi->ch_shift == nullptr))
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: ch_scale and ch_shift go together");
-  if (out == nullptr && epi->codes_a == nullptr && epi->codes_b == nullptr)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: no output requested");
-  if ((out && (uintptr_t)out % 16) || (epi->residual && (uintptr_t)epi->residual % 16))
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: out/residual must be 16-byte aligned");
-  rc = code_target(epi->codes_a, epi->cp_a, epi->sf_a, epi->bits_a, epi->terms_a, cout, "a");
+  rc = apply_epilogue(epi, cout, out, tq::conv_num_configs(), &a);
   if (rc != TQ_OK) return rc;
-  rc = code_target(epi->codes_b, epi->cp_b, epi->sf_b, epi->bits_b, epi->terms_b, cout, "b");
-  if (rc != TQ_OK) return rc;
-  a.ch_scale = epi->ch_scale;
-  a.ch_shift = epi->ch_shift;
-  a.residual = epi->residual;
-  a.relu = epi->relu;
-  a.codes_a = epi->codes_a;
-  a.cp_a = (int)epi->cp_a;
-  a.sf_a = epi->sf_a;
-  a.maxv_a = (float)((1u << (epi->codes_a ? epi->bits_a : 0)) - 1u);
-  a.k_a = epi->terms_a < 0 ? 0 : epi->terms_a;
-  a.codes_b = epi->codes_b;
-  a.cp_b = (int)epi->cp_b;
-  a.sf_b = epi->sf_b;
-  a.maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
-  a.k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
-  if (epi->config < 0 || epi->config > tq::conv_num_configs() || epi->split_k < -1 ||
-      epi->split_k > 64)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
-  if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: workspace must be 16-byte aligned");
-  a.config = epi->config;
-  a.splits = epi->split_k;
-  a.ws = epi->workspace;
-  a.ws_bytes = epi->workspace ? epi->workspace_bytes : 0;
   return hip_status(tq::launch_conv2d_tp(a, 1, (hipStream_t)stream), "conv2d launch");
+}
+
+int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int64_t w,
+                           int64_t cp, const uint16_t* w_codes, int64_t cout, int64_t kh,
+                           int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
+                           int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                           double scale, const float* bias, float* out, int64_t ho, int64_t wo,
+                           int32_t out_nhwc, int32_t kc_steps, const tq_conv_epilogue* epi,
+                           void* stream) {
+  tq::ConvArgs a;
+  int rc = conv_common(reinterpret_cast<const int16_t*>(act_codes), n, h, w, cp,
+                       reinterpret_cast<const int16_t*>(w_codes), cout, kh, kw, kp, stride_h,
+                       stride_w, pad_h, pad_w, dil_h, dil_w, scale, bias, out, ho, wo, &a);
+  if (rc != TQ_OK) return rc;
+  if (kp % 64 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_f16: kp must be a multiple of 64");
+  if (kc_steps < 0) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_f16: kc_steps must be >= 0");
+  a.kc_steps = kc_steps;
+  if (epi == nullptr) {
+    if (out == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: out is null");
+  } else {
+    if (!out_nhwc)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_f16: the fused epilogue is channels_last");
+    if (epi->split_k != 0 && epi->split_k != 1)
+      return fail(TQ_ERR_UNSUPPORTED, "conv2d_f16: the MFMA engine does not split K");
+    rc = apply_epilogue(epi, cout, out, tq::conv_mfma_num_configs(), &a);
+    if (rc != TQ_OK) return rc;
+  }
+  return hip_status(tq::launch_conv2d_mfma(a, out_nhwc, (hipStream_t)stream),
+                    "conv2d_f16 launch");
 }
 
 int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t c,
@@ -301,9 +353,10 @@ int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t
 int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, int64_t c,
                               const float* scale, const float* shift, int32_t k,
                               int32_t stride, int32_t pad, float* out, int64_t ho, int64_t wo,
-                              int16_t* codes_a, int64_t cp_a, float sf_a, int32_t bits_a,
-                              int32_t terms_a, int16_t* codes_b, int64_t cp_b, float sf_b,
-                              int32_t bits_b, int32_t terms_b, void* stream) {
+                              void* codes_a, int64_t cp_a, float sf_a, int32_t bits_a,
+                              int32_t terms_a, int32_t fmt_a, void* codes_b, int64_t cp_b,
+                              float sf_b, int32_t bits_b, int32_t terms_b, int32_t fmt_b,
+                              void* stream) {
   if (n < 0 || h < 1 || w < 1 || c < 8 || c % 8 != 0 || ho < 1 || wo < 1 || k < 1 ||
       stride < 1 || pad < 0 || pad >= k)
     return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: bad shape or pooling window");
@@ -311,9 +364,9 @@ int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, i
     return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: output larger than the input");
   if (!x || !out || !scale || !shift || (uintptr_t)x % 16 || (uintptr_t)out % 16)
     return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: null or misaligned buffer");
-  int rc = code_target(codes_a, cp_a, sf_a, bits_a, terms_a, c, "a");
+  int rc = code_target(codes_a, cp_a, sf_a, bits_a, terms_a, fmt_a, c, "a");
   if (rc != TQ_OK) return rc;
-  rc = code_target(codes_b, cp_b, sf_b, bits_b, terms_b, c, "b");
+  rc = code_target(codes_b, cp_b, sf_b, bits_b, terms_b, fmt_b, c, "b");
   if (rc != TQ_OK) return rc;
   if ((codes_a && (uintptr_t)codes_a % 16) || (codes_b && (uintptr_t)codes_b % 16))
     return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: codes must be 16-byte aligned");
@@ -331,12 +384,14 @@ int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, i
   a.k = k;
   a.s = stride;
   a.pad = pad;
-  a.codes_a = codes_a;
+  a.codes_a = static_cast<int16_t*>(codes_a);
+  a.fmt_a = fmt_a;
   a.cp_a = (int)cp_a;
   a.sf_a = sf_a;
   a.maxv_a = (float)((1u << (codes_a ? bits_a : 0)) - 1u);
   a.k_a = terms_a < 0 ? 0 : terms_a;
-  a.codes_b = codes_b;
+  a.codes_b = static_cast<int16_t*>(codes_b);
+  a.fmt_b = fmt_b;
   a.cp_b = (int)cp_b;
   a.sf_b = sf_b;
   a.maxv_b = (float)((1u << (codes_b ? bits_b : 0)) - 1u);

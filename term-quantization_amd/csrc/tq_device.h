@@ -75,4 +75,15 @@ __device__ __forceinline__ int32_t tr_value_g1(T x, float sf, float maxv, int k)
   return kept_value(pos, neg, keep, x < (T)0);
 }
 
+// Activation / weight code formats of the term-pair kernels (include/tq.h TQ_CODES_*):
+// the same signed integer term sum v stored as int16 (VALU dot2 engine) or as the fp16
+// value v (MFMA engine; exact for |v| <= 2048, i.e. bitwidth <= 11).
+constexpr int kCodesI16 = 0;
+constexpr int kCodesF16 = 1;
+
+__device__ __forceinline__ uint32_t code_bits(int32_t v, int fmt) {
+  return fmt == kCodesF16 ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v)
+                          : ((uint32_t)v & 0xFFFFu);
+}
+
 }  // namespace tq

@@ -1,0 +1,94 @@
+// Epilogue building blocks shared by the term-pair conv kernels (VALU dot2 engine,
+// tr_conv.hip, and MFMA engine, tr_conv_mfma.hip): both finish EXACT integer term-pair sums
+// the same way, so their outputs are bit-identical for the same accumulators.
+//
+//   y = fp32(double(acc) * ch_scale[c] + ch_shift[c])   (conv scale, bias, folded eval BN)
+//     | fp32(double(acc) * scale + bias[c])
+//   y += residual (fp32), relu, fp32 store, next TR layers' activation codes
+//   (tr_layer.py:96-99 applied to y) in the consumer's code format.
+#pragma once
+
+#include "tq_device.h"
+#include "tq_launch.h"
+
+namespace tq {
+namespace {
+
+// Per-channel epilogue coefficients of channels co..co+3: y = acc * sc + sh (fp64).
+__device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4],
+                                          double sh[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = co + i < a.Cout;
+    if (a.ch_scale) {
+      sc[i] = ok ? a.ch_scale[co + i] : 0.0;
+      sh[i] = ok ? a.ch_shift[co + i] : 0.0;
+    } else {
+      sc[i] = a.scale;
+      sh[i] = (a.bias && ok) ? (double)a.bias[co + i] : 0.0;
+    }
+  }
+}
+
+__device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, int co,
+                                             const float y[4], float sf, float maxv, int k,
+                                             int fmt) {
+  uint32_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = code_bits(tr_value_g1(y[i], sf, maxv, k), fmt);
+  *reinterpret_cast<int2*>(codes + p * cp + co) =
+      make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+}
+
+// Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
+// one fp64->fp32 rounding, residual add and ReLU in fp32, fp32 store, next layers' TR codes
+// (tr_layer.py:96-99 applied to the stored value).
+__device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
+                                           const int acc[4], const double sc[4],
+                                           const double sh[4], bool vec) {
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
+  if (a.residual) {
+    const float* r = a.residual + p * a.Cout + co;
+    if (vec) {
+      const float4 rv = *reinterpret_cast<const float4*>(r);
+      y[0] += rv.x;
+      y[1] += rv.y;
+      y[2] += rv.z;
+      y[3] += rv.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (co + i < a.Cout) y[i] += r[i];
+    }
+  }
+  if (a.relu) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+  }
+  if (a.out) {
+    float* dst = a.out + p * a.Cout + co;
+    if (vec) {
+      *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (co + i < a.Cout) dst[i] = y[i];
+    }
+  }
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.sf_a, a.maxv_a, a.k_a, a.fmt_a);
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.sf_b, a.maxv_b, a.k_b, a.fmt_b);
+}
+
+// Bijective XCD-aware remap of the block index: blocks are dealt round-robin to the 8 XCDs
+// (bid % 8), so hand each XCD a contiguous run of logical work items (neighbouring pixel
+// tiles share halo rows, Cout tiles of a pixel tile share its activation tile, both then
+// hit one L2).  Placement is a speed choice only.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+}  // namespace
+}  // namespace tq

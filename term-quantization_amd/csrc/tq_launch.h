@@ -35,6 +35,11 @@ struct ConvArgs {
   int16_t* codes_b;
   int cp_b, k_b;
   float sf_b, maxv_b;
+  int fmt_a, fmt_b;     // code formats of codes_a / codes_b (kCodesI16 / kCodesF16)
+  // MFMA engine only: fp32 accumulators are moved into the int32 sums every kc_steps
+  // K-steps of 64 codes, a window whose |partial sums| the host has bounded by 2^24 (so
+  // every fp32 partial sum is an exact integer); 0 = never needed.
+  int kc_steps;
   // Execution choices: config 0 = heuristic, 1..conv_num_configs() = a fixed tile config;
   // splits: 1 data-parallel, > 1 K-split with int32 atomics into ws ([P][Cout]), -1
   // stream-K (ws holds two BM x BN int32 slabs per resident block); NHWC output only.
@@ -66,13 +71,14 @@ struct PoolArgs {
   int16_t* codes_b;
   int cp_b, k_b;
   float sf_b, maxv_b;
+  int fmt_a, fmt_b;
 };
 
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
 
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
                              int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,
-                             hipStream_t stream);
+                             int fmt, hipStream_t stream);
 
 int conv_tile_m(int64_t cout);
 int conv_num_configs();
@@ -81,5 +87,9 @@ int64_t conv_workspace_bytes(int64_t p, int64_t cout);
 hipError_t launch_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                               int64_t nsf, int bitwidth, int k, double* errs, hipStream_t stream);
 hipError_t launch_conv2d_tp(const ConvArgs& a, int out_nhwc, hipStream_t stream);
+
+// MFMA engine: x, w hold fp16 codes (kCodesF16), Kp % 64 == 0, Cout_pad % 128 == 0.
+hipError_t launch_conv2d_mfma(const ConvArgs& a, int out_nhwc, hipStream_t stream);
+int conv_mfma_num_configs();
 
 }  // namespace tq

@@ -61,15 +61,12 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_encode_kernel(PoolArgs a)
     const float maxv = side ? a.maxv_b : a.maxv_a;
     const int k = side ? a.k_b : a.k_a;
     const int cp = side ? a.cp_b : a.cp_a;
-    int32_t v[8];
+    const int fmt = side ? a.fmt_b : a.fmt_a;
+    uint32_t b[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = tr_value_g1(y[i], sf, maxv, k);
-    int4 packed;
-    packed.x = (v[0] & 0xFFFF) | (v[1] << 16);
-    packed.y = (v[2] & 0xFFFF) | (v[3] << 16);
-    packed.z = (v[4] & 0xFFFF) | (v[5] << 16);
-    packed.w = (v[6] & 0xFFFF) | (v[7] << 16);
-    *reinterpret_cast<int4*>(codes + p * cp + c0) = packed;
+    for (int i = 0; i < 8; ++i) b[i] = code_bits(tr_value_g1(y[i], sf, maxv, k), fmt);
+    *reinterpret_cast<uint4*>(codes + p * cp + c0) = make_uint4(
+        b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
   }
 }
 

@@ -22,6 +22,7 @@
 #include <cmath>
 
 #include "tq_device.h"
+#include "tq_epilogue.h"
 #include "tq_launch.h"
 
 namespace tq {
@@ -31,72 +32,6 @@ namespace {
 __device__ __forceinline__ int dot2(int a, int b, int c) {
   typedef short s2 __attribute__((ext_vector_type(2)));
   return __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, a), __builtin_bit_cast(s2, b), c, false);
-}
-
-// Per-channel epilogue coefficients of channels co..co+3: y = acc * sc + sh (fp64).
-__device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4],
-                                          double sh[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bool ok = co + i < a.Cout;
-    if (a.ch_scale) {
-      sc[i] = ok ? a.ch_scale[co + i] : 0.0;
-      sh[i] = ok ? a.ch_shift[co + i] : 0.0;
-    } else {
-      sc[i] = a.scale;
-      sh[i] = (a.bias && ok) ? (double)a.bias[co + i] : 0.0;
-    }
-  }
-}
-
-__device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, int co,
-                                             const float y[4], float sf, float maxv, int k) {
-  int32_t v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = tr_value_g1(y[i], sf, maxv, k);
-  *reinterpret_cast<int2*>(codes + p * cp + co) =
-      make_int2((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16));
-}
-
-// Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
-// one fp64->fp32 rounding, residual add and ReLU in fp32, fp32 store, next layers' TR codes
-// (tr_layer.py:96-99 applied to the stored value).
-__device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
-                                           const int acc[4], const double sc[4],
-                                           const double sh[4], bool vec) {
-  float y[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
-  if (a.residual) {
-    const float* r = a.residual + p * a.Cout + co;
-    if (vec) {
-      const float4 rv = *reinterpret_cast<const float4*>(r);
-      y[0] += rv.x;
-      y[1] += rv.y;
-      y[2] += rv.z;
-      y[3] += rv.w;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (co + i < a.Cout) y[i] += r[i];
-    }
-  }
-  if (a.relu) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) y[i] = y[i] > 0.0f ? y[i] : 0.0f;
-  }
-  if (a.out) {
-    float* dst = a.out + p * a.Cout + co;
-    if (vec) {
-      *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (co + i < a.Cout) dst[i] = y[i];
-    }
-  }
-  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.sf_a, a.maxv_a, a.k_a);
-  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.sf_b, a.maxv_b, a.k_b);
 }
 
 // LDS image of one K-step (double-buffered): [k-pair][m] and [k-pair][n] dwords.
@@ -291,15 +226,6 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int64_t
   }
 }
 
-// Bijective XCD-aware remap of the block index: blocks are dealt round-robin to the 8 XCDs
-// (bid % 8), so hand each XCD a contiguous run of logical work items (neighbouring pixel
-// tiles share halo rows, Cout tiles of a pixel tile share its activation tile, both then
-// hit one L2).  Placement is a speed choice only.
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-  const int q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
-  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-}
-
 // Data-parallel schedule: one tile (or one K-split of a tile) per block.  SPLIT: the block
 // adds its partial sums into the int32 workspace (exact, order-independent) and
 // conv_finalize_kernel applies the epilogue.
@@ -457,7 +383,8 @@ template <bool IN_NHWC>
 __global__ __launch_bounds__(256) void act_encode_kernel(const float* __restrict__ x,
                                                          int16_t* __restrict__ codes,
                                                          int64_t npix, int64_t HW, int C,
-                                                         int Cp, float sf, float maxv, int k) {
+                                                         int Cp, float sf, float maxv, int k,
+                                                         int fmt) {
   const int chunks = Cp / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= npix * chunks) return;
@@ -483,19 +410,18 @@ __global__ __launch_bounds__(256) void act_encode_kernel(const float* __restrict
       }
     }
   }
-  int4 packed;
-  packed.x = (v[0] & 0xFFFF) | (v[1] << 16);
-  packed.y = (v[2] & 0xFFFF) | (v[3] << 16);
-  packed.z = (v[4] & 0xFFFF) | (v[5] << 16);
-  packed.w = (v[6] & 0xFFFF) | (v[7] << 16);
-  *reinterpret_cast<int4*>(codes + pix * Cp + c0) = packed;
+  uint32_t b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = code_bits(v[i], fmt);
+  *reinterpret_cast<uint4*>(codes + pix * Cp + c0) =
+      make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
 }
 
 }  // namespace
 
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
                              int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,
-                             hipStream_t stream) {
+                             int fmt, hipStream_t stream) {
   const float maxv = (float)((1u << bitwidth) - 1u);
   const int64_t npix = N * H * W;
   const int64_t n = npix * (Cp / 8);
@@ -503,10 +429,10 @@ hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, 
   const dim3 grid((unsigned)((n + 255) / 256));
   if (in_nhwc)
     act_encode_kernel<true><<<grid, 256, 0, stream>>>(x, codes, npix, H * W, (int)C, (int)Cp,
-                                                       sf, maxv, k);
+                                                       sf, maxv, k, fmt);
   else
     act_encode_kernel<false><<<grid, 256, 0, stream>>>(x, codes, npix, H * W, (int)C, (int)Cp,
-                                                        sf, maxv, k);
+                                                        sf, maxv, k, fmt);
   return hipGetLastError();
 }
 

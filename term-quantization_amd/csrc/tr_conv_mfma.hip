@@ -1,0 +1,301 @@
+// Term-pair Conv2d on the CDNA4 matrix cores -- the MFMA engine of the accumulation the
+// reference leaves to a dense fp32 cuDNN conv of fake-quantized tensors (tr_layer.py:124-126).
+//
+// Why a matrix core can do term-pair arithmetic exactly.  A TR'd activation is sf_x * v_x
+// and a TR'd weight sf_w * v_w, v the signed sum of the element's kept HESE terms; the
+// term-pair sum of one output is sum_k v_x[k] * v_w[k] (tr_conv.hip).  Every v with
+// |v| <= 2048 (bitwidth <= 11; ResNet-18 TQ uses 9) is an fp16 value exactly, each product
+// of two is exact in fp32 (|v_x v_w| <= 2^22), and a sum of integers stays exact in fp32 as
+// long as every partial sum is below 2^24 in magnitude -- in any association order, so the
+// order in which v_mfma_f32_32x32x16_f16 adds its products does not matter.  The host bounds
+// sum_{k in window} |v_w[m][k]| * 2^db over every window of `kc_steps` K-steps (64 codes
+// each) of every weight row (tq_ops.mfma_flush_steps); the kernel moves its fp32 accumulators
+// into int32 sums at least that often.  The int32 result is therefore the exact integer
+// term-pair sum, bit-identical to the VALU dot2 engine, and the epilogue (tq_epilogue.h)
+// rounds it once exactly as that engine does.
+//
+// Data layout in HBM (fp16 codes, kCodesF16):
+//   activation codes  [N][H][W][Cp] fp16 (NHWC, channels padded to Cp % 8 == 0 with 0)
+//   weight codes      [Cout_pad][Kp] fp16, k = (kh*KW + kw)*Cp + c, Kp % 64 == 0, zero pad
+//   output            fp32, NHWC (fused epilogue) or NCHW
+//
+// Implicit GEMM: M = Cout, N = output pixels (N*Ho*Wo), K = KH*KW*Cp in K-steps of 64 codes.
+// 256 threads = 4 waves, each wave a 64 x 64 output tile = 2 x 2 MFMA 32x32 blocks; the
+// block tile is 128 x 128 (2 x 2 waves) or 64 x 256 (1 x 4 waves, Cout <= 64).  A K-step
+// stages BM + BN rows x 128 B through LDS (double-buffered, one barrier per step, next
+// step's 16-B global loads in flight during the current step's 16 MFMAs per wave).  LDS rows
+// are 8 chunks of 16 B with chunk' = chunk ^ ((row >> 1) & 7): the MFMA fragment reads (32
+// rows at one chunk per half-wave) and the staging writes (2 rows x 8 chunks per 16 lanes)
+// are both bank-conflict free.
+#include "tq_device.h"
+#include "tq_epilogue.h"
+#include "tq_launch.h"
+
+namespace tq {
+
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float float16v __attribute__((ext_vector_type(16)));
+
+constexpr int kKStep = 64;  // codes per K-step
+
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * 8 + (chunk ^ ((row >> 1) & 7));
+}
+
+template <int BM, int BN>
+struct MfmaSmem {
+  uint4 As[2][BM * 8];
+  uint4 Bs[2][BN * 8];
+};
+
+// Accumulator state of one wave: 2 x 2 blocks of 32 x 32, fp32 (exact window) + int32.
+struct MfmaAcc {
+  float16v f[2][2];
+  int i[2][2][16];
+};
+
+__device__ __forceinline__ void acc_zero(MfmaAcc& acc) {
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc.f[bm][bn][r] = 0.0f;
+        acc.i[bm][bn][r] = 0;
+      }
+    }
+}
+
+// fp32 partial sums are exact integers below 2^24: move them into the int32 sums.
+__device__ __forceinline__ void acc_flush(MfmaAcc& acc) {
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc.i[bm][bn][r] += (int)acc.f[bm][bn][r];
+        acc.f[bm][bn][r] = 0.0f;
+      }
+    }
+}
+
+// K-steps [k_begin, k_end) of block tile (m0, n0) into acc.  Ends on a barrier.
+template <int BM, int BN>
+__device__ __forceinline__ void mfma_mainloop(const ConvArgs& a, int m0, int64_t n0,
+                                              int k_begin, int k_end, MfmaAcc& acc,
+                                              MfmaSmem<BM, BN>& sm) {
+  constexpr int WN = BN / 64;  // waves along N
+  constexpr int A_ROWS = BM / 32;
+  constexpr int B_ROWS = BN / 32;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = (wave / WN) * 64;
+  const int wn = (wave % WN) * 64;
+  // staging geometry: this thread moves chunk `ch` (8 codes) of rows r0 + 32 i
+  const int ch = tid & 7;
+  const int r0 = tid >> 3;
+  const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
+  const uint16_t* __restrict__ wg = reinterpret_cast<const uint16_t*>(a.w);
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+
+  int64_t pbase[B_ROWS];
+  int ih0[B_ROWS], iw0[B_ROWS];
+#pragma unroll
+  for (int r = 0; r < B_ROWS; ++r) {
+    const int64_t p = n0 + r0 + 32 * r;
+    if (p < a.P) {
+      const int64_t img = p / HoWo;
+      const int64_t rem = p - img * HoWo;
+      const int oh = (int)(rem / a.Wo);
+      const int ow = (int)(rem - (int64_t)oh * a.Wo);
+      ih0[r] = oh * a.sh - a.ph;
+      iw0[r] = ow * a.sw - a.pw;
+      pbase[r] = img * a.H;
+    } else {
+      ih0[r] = -(1 << 28);  // never in bounds
+      iw0[r] = 0;
+      pbase[r] = 0;
+    }
+  }
+  int ktap, kc, kr, ks;
+  {
+    const int k0 = k_begin * kKStep + ch * 8;
+    ktap = k0 / a.Cp;
+    kc = k0 - ktap * a.Cp;
+    kr = ktap / a.KW;
+    ks = ktap - kr * a.KW;
+  }
+  const uint16_t* __restrict__ wrow[A_ROWS];
+#pragma unroll
+  for (int r = 0; r < A_ROWS; ++r)
+    wrow[r] = wg + (int64_t)(m0 + r0 + 32 * r) * a.Kp + (int64_t)k_begin * kKStep + ch * 8;
+  const int ntaps = a.KH * a.KW;
+  const int nsteps = k_end - k_begin;
+
+  uint4 ra[A_ROWS], rb[B_ROWS];
+  auto load_tile = [&](int step) {
+#pragma unroll
+    for (int r = 0; r < A_ROWS; ++r)
+      ra[r] = *reinterpret_cast<const uint4*>(wrow[r] + (int64_t)step * kKStep);
+#pragma unroll
+    for (int r = 0; r < B_ROWS; ++r) {
+      rb[r] = make_uint4(0, 0, 0, 0);
+      if (ktap < ntaps) {
+        const int ih = ih0[r] + kr * a.dh;
+        const int iw = iw0[r] + ks * a.dw;
+        if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+          rb[r] = *reinterpret_cast<const uint4*>(xg + ((pbase[r] + ih) * a.W + iw) * a.Cp + kc);
+      }
+    }
+    kc += kKStep;
+    while (kc >= a.Cp) {
+      kc -= a.Cp;
+      ++ktap;
+      if (++ks == a.KW) {
+        ks = 0;
+        ++kr;
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < A_ROWS; ++r) sm.As[buf][swz(r0 + 32 * r, ch)] = ra[r];
+#pragma unroll
+    for (int r = 0; r < B_ROWS; ++r) sm.Bs[buf][swz(r0 + 32 * r, ch)] = rb[r];
+  };
+
+  if (nsteps <= 0) return;
+  const int r32 = lane & 31;
+  const int hh = lane >> 5;
+  const int kc_steps = a.kc_steps > 0 ? a.kc_steps : (1 << 30);
+  int since_flush = 0;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) load_tile(step + 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + hh;
+      half8 af[2], bf[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        af[b] = __builtin_bit_cast(half8, sm.As[cur][swz(wm + 32 * b + r32, c)]);
+        bf[b] = __builtin_bit_cast(half8, sm.Bs[cur][swz(wn + 32 * b + r32, c)]);
+      }
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          acc.f[bm][bn] =
+              __builtin_amdgcn_mfma_f32_32x32x16_f16(af[bm], bf[bn], acc.f[bm][bn], 0, 0, 0);
+    }
+    if (++since_flush == kc_steps) {
+      acc_flush(acc);
+      since_flush = 0;
+    }
+    if (step + 1 < nsteps) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+  acc_flush(acc);
+}
+
+// Epilogue: lane (r32, hh) of a 32x32 block holds pixel column r32 and Cout rows
+// 8*(reg>>2) + 4*hh + (reg&3), i.e. 4 consecutive channels per register quad.
+template <int BM, int BN, bool OUT_NHWC>
+__device__ __forceinline__ void mfma_epilogue(const ConvArgs& a, int m0, int64_t n0,
+                                              const MfmaAcc& acc) {
+  constexpr int WN = BN / 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave / WN) * 64;
+  const int wn = (wave % WN) * 64;
+  const int r32 = lane & 31;
+  const int hh = lane >> 5;
+  if (OUT_NHWC) {
+    const bool vec = (a.Cout & 3) == 0;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = m0 + wm + 32 * bm + 8 * q + 4 * hh;
+        if (co >= a.Cout) continue;
+        double sc[4], sh[4];
+        load_coef(a, co, sc, sh);
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) {
+          const int64_t p = n0 + wn + 32 * bn + r32;
+          if (p >= a.P) continue;
+          const int acc4[4] = {acc.i[bm][bn][4 * q], acc.i[bm][bn][4 * q + 1],
+                               acc.i[bm][bn][4 * q + 2], acc.i[bm][bn][4 * q + 3]};
+          emit4_nhwc(a, p, co, acc4, sc, sh, vec);
+        }
+      }
+    }
+  } else {
+    const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+      const int64_t p = n0 + wn + 32 * bn + r32;
+      if (p >= a.P) continue;
+      const int64_t img = p / HoWo;
+      const int64_t rem = p - img * HoWo;
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = m0 + wm + 32 * bm + 8 * (r >> 2) + 4 * hh + (r & 3);
+          if (co >= a.Cout) continue;
+          const double sh = a.bias ? (double)a.bias[co] : 0.0;
+          a.out[(img * a.Cout + co) * HoWo + rem] =
+              (float)((double)acc.i[bm][bn][r] * a.scale + sh);
+        }
+    }
+  }
+}
+
+template <int BM, int BN, bool OUT_NHWC>
+__global__ __launch_bounds__(256, 2) void conv2d_tp_mfma_kernel(ConvArgs a) {
+  static_assert((BM / 64) * (BN / 64) == 4, "4 waves of 64 x 64");
+  __shared__ __attribute__((aligned(16))) MfmaSmem<BM, BN> sm;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int m0 = (tile % mt) * BM;
+  const int64_t n0 = (int64_t)(tile / mt) * BN;
+  MfmaAcc acc;
+  acc_zero(acc);
+  mfma_mainloop<BM, BN>(a, m0, n0, 0, a.Kp / kKStep, acc, sm);
+  mfma_epilogue<BM, BN, OUT_NHWC>(a, m0, n0, acc);
+}
+
+template <int BM, int BN>
+hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) {
+  const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + BM - 1) / BM);
+  const dim3 grid((unsigned)tiles);
+  if (out_nhwc)
+    conv2d_tp_mfma_kernel<BM, BN, true><<<grid, 256, 0, stream>>>(a);
+  else
+    conv2d_tp_mfma_kernel<BM, BN, false><<<grid, 256, 0, stream>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int conv_mfma_num_configs() { return 2; }
+
+hipError_t launch_conv2d_mfma(const ConvArgs& a, int out_nhwc, hipStream_t stream) {
+  if (a.P == 0 || a.Cout == 0) return hipSuccess;
+  int cfg = a.config > 0 ? a.config - 1 : (a.Cout <= 64 ? 1 : 0);
+  switch (cfg) {
+    case 0: return launch_mfma_cfg<128, 128>(a, out_nhwc, stream);
+    default: return launch_mfma_cfg<64, 256>(a, out_nhwc, stream);
+  }
+}
+
+}  // namespace tq

@@ -5,7 +5,7 @@ every op as its own pass over HBM: term-pair conv -> BN -> ReLU -> (+identity ->
 the next layer's activation TR.  This executor runs the same math with each block's ops
 folded into the term-pair kernel's epilogue (tq_conv2d_termpair_fused):
 
-  conv1:       codes(x; sf1)   -> TR(relu(bn1(conv1)); sf2) as int16 codes   (no fp32 tensor)
+  conv1:       codes(x; sf1)   -> TR(relu(bn1(conv1)); sf2) as codes         (no fp32 tensor)
   downsample:  codes(x; sf_d)  -> bn_d(conv_d) fp32                          (the identity)
   conv2:       codes(mid; sf2) -> y = relu(bn2(conv2) + identity) fp32, plus
                                   TR(y; sf of the next block's conv1 / downsample) codes
@@ -55,6 +55,8 @@ class _Conv(object):
         self.cp_in = layer.act_channels
         self.quant = (layer.input_quant.sf, layer.data_bits, layer.data_terms)
         self.scale, self.shift = _fold_bn(layer, bn)
+        self.code_dtype = layer.w_codes.dtype   # int16 (VALU engine) / float16 (MFMA engine)
+        self.kc_steps = layer.kc_steps
         if self.cout % 4:
             raise ValueError("fused epilogue needs Cout % 4 == 0")
 
@@ -70,9 +72,9 @@ class _Conv(object):
         dev = codes.device
         ca = cb = None
         if next_a is not None:
-            ca = torch.empty((n, ho, wo, next_a.cp_in), dtype=torch.int16, device=dev)
+            ca = torch.empty((n, ho, wo, next_a.cp_in), dtype=next_a.code_dtype, device=dev)
         if next_b is not None:
-            cb = torch.empty((n, ho, wo, next_b.cp_in), dtype=torch.int16, device=dev)
+            cb = torch.empty((n, ho, wo, next_b.cp_in), dtype=next_b.code_dtype, device=dev)
         if out is True:
             out = torch.empty((n, self.cout, ho, wo), dtype=torch.float32, device=dev,
                               memory_format=torch.channels_last)
@@ -89,7 +91,8 @@ class _Conv(object):
                 self.padding, self.dilation, ho, wo, out=out, ch_scale=self.scale,
                 ch_shift=self.shift, residual=res, relu=relu, codes_a=ca,
                 quant_a=next_a.quant if next_a else None, codes_b=cb,
-                quant_b=next_b.quant if next_b else None, workspace=ws))
+                quant_b=next_b.quant if next_b else None, workspace=ws,
+                kc_steps=self.kc_steps))
         return out, ca, cb
 
 
@@ -136,12 +139,14 @@ class FusedResNet(nn.Module):
             x = m.maxpool(m.relu(m.bn1(m.conv1(x)))).contiguous(
                 memory_format=torch.channels_last)
             codes = torch.empty((x.shape[0], x.shape[2], x.shape[3], first.conv1.cp_in),
-                                dtype=torch.int16, device=x.device)
+                                dtype=first.conv1.code_dtype, device=x.device)
             tq_ops._launch("act_encode", 4 * x.numel() + 2 * codes.numel(),
                            lambda: tq_native.act_encode(x, True, *first.conv1.quant, codes))
             codes_down = None
             if first.down is not None:
-                codes_down = torch.empty_like(codes)
+                codes_down = torch.empty((x.shape[0], x.shape[2], x.shape[3],
+                                          first.down.cp_in), dtype=first.down.code_dtype,
+                                         device=x.device)
                 tq_native.act_encode(x, True, *first.down.quant, codes_down)
             return x, codes, codes_down
         y = m.conv1(x).contiguous(memory_format=torch.channels_last)
@@ -150,10 +155,11 @@ class FusedResNet(nn.Module):
         ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         out = torch.empty((n, c, ho, wo), dtype=torch.float32, device=y.device,
                           memory_format=torch.channels_last)
-        codes = torch.empty((n, ho, wo, first.conv1.cp_in), dtype=torch.int16, device=y.device)
+        codes = torch.empty((n, ho, wo, first.conv1.cp_in), dtype=first.conv1.code_dtype,
+                            device=y.device)
         codes_down = None
         if first.down is not None:
-            codes_down = torch.empty((n, ho, wo, first.down.cp_in), dtype=torch.int16,
+            codes_down = torch.empty((n, ho, wo, first.down.cp_in), dtype=first.down.code_dtype,
                                      device=y.device)
         tq_ops._launch(
             "stem_pool_encode", 4 * y.numel() + 4 * out.numel() + 2 * codes.numel(),

@@ -34,7 +34,8 @@ _SIGNATURES = {
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
                          _vp],
-    "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _vp],
+    "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _i32,
+                      _vp],
     "tq_conv2d_cout_align": [],
     "tq_conv2d_num_configs": [],
     "tq_conv2d_workspace_bytes": [_i64, _i64],
@@ -43,8 +44,9 @@ _SIGNATURES = {
                            _vp],
     "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
     "tq_bn_relu_maxpool_encode": [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _i32, _i32,
-                                  _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _vp, _i64,
-                                  _f32, _i32, _i32, _vp],
+                                  _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _i32, _vp,
+                                  _i64, _f32, _i32, _i32, _i32, _vp],
+    "tq_conv2d_mfma_num_configs": [],
     "tq_dwconv2d_termpair": [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                              _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32, _vp],
 }
@@ -57,15 +59,34 @@ class ConvEpilogue(ctypes.Structure):
                 ("codes_b", _vp), ("cp_b", _i64), ("sf_b", _f32), ("bits_b", _i32),
                 ("terms_b", _i32),
                 ("workspace", _vp), ("workspace_bytes", _i64), ("split_k", _i32),
-                ("config", _i32)]
+                ("config", _i32), ("fmt_a", _i32), ("fmt_b", _i32)]
 
 
 _SIGNATURES["tq_conv2d_termpair_fused"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
     _i64, _f64, _vp, _vp, _i64, _i64, ctypes.POINTER(ConvEpilogue), _vp]
 
+_SIGNATURES["tq_conv2d_termpair_f16"] = [
+    _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+    _i64, _f64, _vp, _vp, _i64, _i64, _i32, _i32, ctypes.POINTER(ConvEpilogue), _vp]
+
+# include/tq.h TQ_CODES_*: the code format follows the code tensor's dtype
+CODES_I16 = 0
+CODES_F16 = 1
+
+
+def code_format(codes):
+    """TQ_CODES_* of a code tensor: int16 -> TQ_CODES_I16, float16 -> TQ_CODES_F16."""
+    if codes.dtype == torch.int16:
+        return CODES_I16
+    if codes.dtype == torch.float16:
+        return CODES_F16
+    raise RuntimeError("term-pair codes must be int16 or float16 (got %s)" % codes.dtype)
+
+
 _RESTYPE = {"tq_version": ctypes.c_char_p, "tq_last_error": ctypes.c_char_p,
             "tq_conv2d_cout_align": _i64, "tq_conv2d_num_configs": _i32,
+            "tq_conv2d_mfma_num_configs": _i32,
             "tq_conv2d_workspace_bytes": _i64}
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -130,10 +151,12 @@ def tr_into(inp, out, sf, bitwidth, group_size, num_keep_terms, codes=None):
 
 
 def act_encode(x, in_nhwc, sf, bitwidth, num_keep_terms, codes):
+    """TR of x into NHWC codes; int16 ``codes`` for the VALU engine, float16 for MFMA."""
     n, c, h, w = x.shape
+    fmt = code_format(codes)
     with torch.cuda.device(x.device):
         rc = lib().tq_act_encode(_ptr(x), int(in_nhwc), n, c, h, w, sf, bitwidth,
-                                 num_keep_terms, _ptr(codes), codes.shape[-1], _stream(x))
+                                 num_keep_terms, _ptr(codes), codes.shape[-1], fmt, _stream(x))
     _check(rc)
     return codes
 
@@ -143,15 +166,27 @@ def conv2d_cout_align():
 
 
 def conv2d_termpair(codes, w_codes, cout, kh, kw, stride, padding, dilation, scale, bias, out,
-                    out_nhwc):
+                    out_nhwc, kc_steps=0):
+    """Plain term-pair conv.  int16 codes run the VALU engine (tq_conv2d_termpair), float16
+    codes the MFMA engine (tq_conv2d_termpair_f16, flush interval ``kc_steps``)."""
     n, h, w, cp = codes.shape
     ho, wo = out.shape[2], out.shape[3]
+    fmt = code_format(codes)
+    if code_format(w_codes) != fmt:
+        raise RuntimeError("activation and weight codes must have the same format")
     with torch.cuda.device(codes.device):
-        rc = lib().tq_conv2d_termpair(_ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw,
-                                      w_codes.shape[1], stride[0], stride[1], padding[0],
-                                      padding[1], dilation[0], dilation[1], float(scale),
-                                      _ptr(bias), _ptr(out), ho, wo, int(out_nhwc),
-                                      _stream(codes))
+        if fmt == CODES_F16:
+            rc = lib().tq_conv2d_termpair_f16(
+                _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],
+                stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1],
+                float(scale), _ptr(bias), _ptr(out), ho, wo, int(out_nhwc), int(kc_steps), None,
+                _stream(codes))
+        else:
+            rc = lib().tq_conv2d_termpair(_ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh,
+                                          kw, w_codes.shape[1], stride[0], stride[1],
+                                          padding[0], padding[1], dilation[0], dilation[1],
+                                          float(scale), _ptr(bias), _ptr(out), ho, wo,
+                                          int(out_nhwc), _stream(codes))
     _check(rc)
     return out
 
@@ -169,28 +204,41 @@ def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
 def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilation, ho, wo,
                           out=None, ch_scale=None, ch_shift=None, residual=None, relu=False,
                           codes_a=None, quant_a=None, codes_b=None, quant_b=None,
-                          workspace=None, split_k=0, config=0):
+                          workspace=None, split_k=0, config=0, kc_steps=0):
     """Term-pair conv with the fused epilogue of tq_conv2d_termpair_fused (channels_last).
-    quant_a/_b = (sf, bits, terms) of the layer consuming codes_a/_b.  ``workspace`` (int32,
-    >= n*ho*wo*cout elements) lets the kernel split the K loop over workgroups."""
+    quant_a/_b = (sf, bits, terms) of the layer consuming codes_a/_b, whose dtype (int16 /
+    float16) is that layer's code format.  ``workspace`` (int32, >= n*ho*wo*cout elements)
+    lets the VALU kernel split the K loop over workgroups.  float16 input codes run the MFMA
+    engine (tq_conv2d_termpair_f16) with flush interval ``kc_steps``."""
     n, h, w, cp = codes.shape
+    fmt = code_format(codes)
+    if code_format(w_codes) != fmt:
+        raise RuntimeError("activation and weight codes must have the same format")
     epi = ConvEpilogue()
     epi.ch_scale, epi.ch_shift = _ptr(ch_scale), _ptr(ch_shift)
     epi.residual, epi.relu = _ptr(residual), int(bool(relu))
     if codes_a is not None:
         epi.codes_a, epi.cp_a = _ptr(codes_a), codes_a.shape[-1]
         epi.sf_a, epi.bits_a, epi.terms_a = float(quant_a[0]), int(quant_a[1]), int(quant_a[2])
+        epi.fmt_a = code_format(codes_a)
     if codes_b is not None:
         epi.codes_b, epi.cp_b = _ptr(codes_b), codes_b.shape[-1]
         epi.sf_b, epi.bits_b, epi.terms_b = float(quant_b[0]), int(quant_b[1]), int(quant_b[2])
+        epi.fmt_b = code_format(codes_b)
     epi.workspace, epi.split_k, epi.config = _ptr(workspace), int(split_k), int(config)
     epi.workspace_bytes = workspace.numel() * workspace.element_size() if workspace is not None \
         else 0
     with torch.cuda.device(codes.device):
-        rc = lib().tq_conv2d_termpair_fused(
-            _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1], stride[0],
-            stride[1], padding[0], padding[1], dilation[0], dilation[1], 0.0, None, _ptr(out),
-            ho, wo, ctypes.byref(epi), _stream(codes))
+        if fmt == CODES_F16:
+            rc = lib().tq_conv2d_termpair_f16(
+                _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],
+                stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1], 0.0,
+                None, _ptr(out), ho, wo, 1, int(kc_steps), ctypes.byref(epi), _stream(codes))
+        else:
+            rc = lib().tq_conv2d_termpair_fused(
+                _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],
+                stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1], 0.0,
+                None, _ptr(out), ho, wo, ctypes.byref(epi), _stream(codes))
     _check(rc)
 
 
@@ -226,8 +274,9 @@ def bn_relu_maxpool_encode(x, scale, shift, k, stride, pad, out, codes_a=None, q
         rc = lib().tq_bn_relu_maxpool_encode(
             _ptr(x), n, h, w, c, _ptr(scale), _ptr(shift), k, stride, pad, _ptr(out), ho, wo,
             _ptr(codes_a), codes_a.shape[-1] if codes_a is not None else 0, float(qa[0]),
-            int(qa[1]), int(qa[2]), _ptr(codes_b),
-            codes_b.shape[-1] if codes_b is not None else 0, float(qb[0]), int(qb[1]),
-            int(qb[2]), _stream(x))
+            int(qa[1]), int(qa[2]), code_format(codes_a) if codes_a is not None else 0,
+            _ptr(codes_b), codes_b.shape[-1] if codes_b is not None else 0, float(qb[0]),
+            int(qb[1]), int(qb[2]), code_format(codes_b) if codes_b is not None else 0,
+            _stream(x))
     _check(rc)
     return out

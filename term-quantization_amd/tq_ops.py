@@ -3,8 +3,15 @@
   tr(input, sf, bitwidth, group_size, num_keep_terms)     reference tr_cuda.tr, same contract
   tr_elementwise(x, sf, bitwidth, num_keep_terms)          group_size-1 TR of any dense layout
   tr_encode(w, sf, bitwidth, group_size, num_keep_terms)   TR(w) plus its integer term sums
-  pack_conv_weight(codes)                                  [O,I,KH,KW] int32 -> [O_pad, Kp] int16
+  conv_engine(data_bits, weight_bits)                      "mfma" (fp16 codes) or "valu" (int16)
+  pack_conv_weight(codes, engine)                          [O,I,KH,KW] int32 -> [O_pad, Kp] codes
+  mfma_flush_steps(packed, data_bits)                      exactness window of the MFMA engine
   tr_conv2d(x, ...)                                        conv2d(TR(x), TR(w)) by term pairs
+
+Two engines accumulate the same exact integer term-pair sums: the VALU engine (int16 codes,
+v_dot2c_i32_i16) and the MFMA engine (fp16 codes, v_mfma_f32_32x32x16_f16 with exact fp32
+windows flushed into int32, csrc/tr_conv_mfma.hip).  Their outputs are bit-identical; a
+layer uses MFMA when its codes fit fp16 exactly (bitwidths <= 11) unless TQ_CONV_ENGINE=valu.
 
 Errors mirror the reference boundary (kernels/tr_cuda.cpp:12-18): RuntimeError for a non-CUDA
 or non-contiguous input, a RuntimeError for an unsupported dtype, IndexError for < 2 dims.
@@ -14,9 +21,14 @@ import torch
 
 import tq_native
 
-ACT_CHANNEL_ALIGN = 8   # int16 codes per 16-byte vector
-K_ALIGN = 32            # codes per K-step of the term-pair kernel
+import os
+
+ACT_CHANNEL_ALIGN = 8   # 16-bit codes per 16-byte vector
+K_ALIGN = 32            # codes per K-step of the VALU term-pair kernel
+K_ALIGN_MFMA = 64       # codes per K-step of the MFMA term-pair kernel
 MAX_CODE_BITS = 14      # |code| <= 2^bitwidth must fit int16
+MAX_F16_CODE_BITS = 11  # |code| <= 2048: every integer is an fp16 value
+FP32_EXACT = 2**24      # integers up to here are exact fp32 values
 
 _kernel_hook = None
 
@@ -104,8 +116,27 @@ def act_channels(c):
     return round_up(c, ACT_CHANNEL_ALIGN)
 
 
-def pack_conv_weight(codes):
-    """[O, I, KH, KW] int32 term sums -> int16 [O_pad, Kp] with k = (kh*KW + kw)*Cp + c.
+def conv_engine(data_bits, weight_bits):
+    """Term-pair engine for a layer: "mfma" when activation and weight codes are exact fp16
+    values (both bitwidths <= 11), else "valu".  TQ_CONV_ENGINE=valu forces the VALU engine
+    (the two are bit-identical; tests compare them)."""
+    forced = os.environ.get("TQ_CONV_ENGINE", "").lower()
+    if forced not in ("", "mfma", "valu"):
+        raise RuntimeError("TQ_CONV_ENGINE must be 'mfma' or 'valu' (got %r)" % forced)
+    if forced == "valu":
+        return "valu"
+    if max(int(data_bits), int(weight_bits)) <= MAX_F16_CODE_BITS:
+        return "mfma"
+    return "valu"
+
+
+def code_dtype(engine):
+    return torch.float16 if engine == "mfma" else torch.int16
+
+
+def pack_conv_weight(codes, engine="valu"):
+    """[O, I, KH, KW] int32 term sums -> [O_pad, Kp] codes with k = (kh*KW + kw)*Cp + c:
+    int16 with Kp % 32 == 0 (VALU engine) or float16 with Kp % 64 == 0 (MFMA engine).
 
     Layout plumbing done once per layer at construction; returns (packed, Cp)."""
     o, i, kh, kw = codes.shape
@@ -114,11 +145,38 @@ def pack_conv_weight(codes):
     if cp != i:
         t = torch.nn.functional.pad(t, (0, cp - i))
     t = t.reshape(o, kh * kw * cp)
-    kp = round_up(kh * kw * cp, K_ALIGN)
+    kp = round_up(kh * kw * cp, K_ALIGN_MFMA if engine == "mfma" else K_ALIGN)
     o_pad = round_up(o, tq_native.conv2d_cout_align())
-    packed = torch.zeros((o_pad, kp), dtype=torch.int16, device=codes.device)
-    packed[:o, :kh * kw * cp] = t.to(torch.int16)
+    dtype = code_dtype(engine)
+    if engine == "mfma" and codes.numel() and codes.abs().max().item() > 2**MAX_F16_CODE_BITS:
+        raise RuntimeError("pack_conv_weight: codes exceed the exact fp16 range")
+    packed = torch.zeros((o_pad, kp), dtype=dtype, device=codes.device)
+    packed[:o, :kh * kw * cp] = t.to(dtype)
     return packed.contiguous(), cp
+
+
+def mfma_flush_steps(packed, data_bits):
+    """Exactness window of the MFMA engine for fp16 weight codes ``packed`` [O_pad, Kp]
+    against activation codes of ``data_bits`` bits (|v_x| <= 2^data_bits).
+
+    Returns the largest n such that every window of n consecutive K-steps (64 codes) of every
+    row satisfies 2^data_bits * sum|v_w| <= 2^24 -- then every fp32 partial sum inside the
+    window is an exact integer -- as the kernel's flush interval: 0 if the whole K range
+    qualifies (no flush needed), -1 if not even one K-step does (the layer must use the VALU
+    engine)."""
+    o_pad, kp = packed.shape
+    steps = packed.double().abs().view(o_pad, kp // K_ALIGN_MFMA, K_ALIGN_MFMA).sum(-1)
+    s = steps.shape[1]
+    lim = float(FP32_EXACT) / float(2**int(data_bits))
+    c = torch.nn.functional.pad(steps.cumsum(1), (1, 0))  # [O_pad, S + 1]
+    best = 0
+    for n in range(1, s + 1):
+        if (c[:, n:] - c[:, :s + 1 - n]).max().item() > lim:
+            break
+        best = n
+    if best == 0:
+        return -1
+    return 0 if best == s else best
 
 
 def conv_out_size(h, k, s, p, d):
@@ -126,11 +184,13 @@ def conv_out_size(h, k, s, p, d):
 
 
 def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_channels,
-              kernel_size, stride, padding, dilation):
+              kernel_size, stride, padding, dilation, kc_steps=0):
     """conv2d(TR(x), TR(w)) + bias by exact term-pair accumulation (groups = 1).
 
     x: fp32 [N, C, H, W] CUDA tensor, NCHW-contiguous or channels_last.  The output has the
-    conv's shape and the input's memory format (as cuDNN/MIOpen convs do)."""
+    conv's shape and the input's memory format (as cuDNN/MIOpen convs do).  The engine
+    follows ``w_packed``'s dtype (pack_conv_weight): float16 -> MFMA with flush interval
+    ``kc_steps`` (mfma_flush_steps), int16 -> VALU."""
     if not x.is_cuda:
         raise RuntimeError("input must be a CUDA tensor")
     if x.dtype != torch.float32 or x.dim() != 4:
@@ -144,7 +204,7 @@ def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_chan
     kh, kw = kernel_size
     ho = conv_out_size(h, kh, stride[0], padding[0], dilation[0])
     wo = conv_out_size(w, kw, stride[1], padding[1], dilation[1])
-    codes = torch.empty((n, h, w, cp), dtype=torch.int16, device=x.device)
+    codes = torch.empty((n, h, w, cp), dtype=w_packed.dtype, device=x.device)
     _launch("act_encode", 4 * n * c * h * w + 2 * n * h * w * cp,
             lambda: tq_native.act_encode(x, nhwc, float(sf_x), int(data_bits), int(data_terms),
                                          codes))
@@ -157,7 +217,8 @@ def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_chan
         bias = bias.detach().to(torch.float32).contiguous()
     _launch("conv2d_termpair", n * ho * wo * out_channels * c * kh * kw,
             lambda: tq_native.conv2d_termpair(codes, w_packed, out_channels, kh, kw, stride,
-                                              padding, dilation, scale, bias, out, nhwc))
+                                              padding, dilation, scale, bias, out, nhwc,
+                                              kc_steps))
     return out
 
 
@@ -214,7 +275,8 @@ def tr_dwconv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, channe
     return out
 
 
-def tr_linear(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features):
+def tr_linear(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features,
+              kc_steps=0):
     """linear(TR(x), TR(w)) + bias by exact term-pair accumulation: the rows of x are the
     pixels of a 1x1 term-pair conv (channels_last [M, C, 1, 1] is x's own memory)."""
     shape = x.shape
@@ -222,5 +284,5 @@ def tr_linear(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_feat
     m = x2.shape[0]
     xc = x2.view(m, 1, 1, shape[-1]).permute(0, 3, 1, 2)  # channels_last view, no copy
     y = tr_conv2d(xc, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features,
-                  (1, 1), (1, 1), (0, 0), (1, 1))
+                  (1, 1), (1, 1), (0, 0), (1, 1), kc_steps)
     return y.permute(0, 2, 3, 1).reshape(*shape[:-1], out_features)

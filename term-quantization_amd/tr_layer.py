@@ -142,6 +142,20 @@ class LinearQuantize(nn.Module):
         self.tracking = False
 
 
+def _pack_termpair(codes, data_bits, weight_bits):
+    """Pack int32 weight term sums [O, I, KH, KW] for the layer's term-pair engine:
+    (packed, Cp, engine, kc_steps).  MFMA when the codes are exact fp16 values and one K-step
+    of products stays inside fp32's exact-integer range, else VALU (int16)."""
+    engine = tq_ops.conv_engine(data_bits, weight_bits)
+    if engine == "mfma":
+        packed, cp = tq_ops.pack_conv_weight(codes, "mfma")
+        kc = tq_ops.mfma_flush_steps(packed, data_bits)
+        if kc >= 0:
+            return packed, cp, "mfma", kc
+    packed, cp = tq_ops.pack_conv_weight(codes, "valu")
+    return packed, cp, "valu", 0
+
+
 def _w_sf(w, weight_bits):
     max_wq = 2**(weight_bits - 1)
     return w.abs().max().item() / max_wq
@@ -158,7 +172,9 @@ class TRConv2dLayer(nn.Module):
     forward: while tracking, ``self.conv`` on the unquantized input (the reference returns x
     from the quantizer while tracking); afterwards conv2d(TR(x), TR(w)) + bias by exact
     term-pair accumulation -- ``self.mode``:
-      "termpair"   groups == 1, data/weight bits <= 14 (int16 codes): tq_ops.tr_conv2d
+      "termpair"   groups == 1, data/weight bits <= 14: tq_ops.tr_conv2d on the MFMA engine
+                   (fp16 codes, bits <= 11; ``self.engine`` "mfma") or the VALU engine
+                   (int16 codes, ``self.engine`` "valu") -- bit-identical results
       "depthwise"  groups == C_in == C_out, weight bits <= 22: tq_ops.tr_dwconv2d
       "reference"  anything else: the reference composition self.conv(self.input_quant(x))
                    with the HIP TR op (``self.termpair`` is True only for "termpair")."""
@@ -194,13 +210,16 @@ class TRConv2dLayer(nn.Module):
             if bound >= 2**31:
                 mode = "reference"
             elif mode == "termpair":
-                packed, cp = tq_ops.pack_conv_weight(codes)
+                packed, cp, self.engine, self.kc_steps = _pack_termpair(codes, data_bits,
+                                                                        weight_bits)
             else:
                 packed, cp = tq_ops.pack_dw_weight(codes)
         else:
             wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
         self.mode = mode
         self.termpair = mode == "termpair"
+        if not self.termpair:
+            self.engine, self.kc_steps = None, 0
         self.register_buffer('w_codes', packed)
         if packed is not None:
             self.act_channels = cp
@@ -223,7 +242,8 @@ class TRConv2dLayer(nn.Module):
             x = torch.nn.functional.pad(x, (pad[2], pad[3], pad[0], pad[1]))
         return tq_ops.tr_conv2d(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, c.bias,
-                                c.out_channels, c.kernel_size, c.stride, c.padding, c.dilation)
+                                c.out_channels, c.kernel_size, c.stride, c.padding, c.dilation,
+                                self.kc_steps)
 
     def tracking(self, tracking):
         if not tracking:
@@ -258,6 +278,7 @@ class TRLinearLayer(nn.Module):
         w = linear_layer.weight
         self.w_sf = _w_sf(w, weight_bits)
         self.termpair = False
+        self.engine, self.kc_steps = None, 0
         packed = None
         if (quantize_input and weight_bits <= tq_ops.MAX_CODE_BITS
                 and data_bits <= tq_ops.MAX_CODE_BITS and w.dtype == torch.float32):
@@ -265,7 +286,8 @@ class TRLinearLayer(nn.Module):
                                          group_size, num_terms)
             bound = codes.abs().to(torch.int64).sum(1).max().item() << data_bits
             if bound < 2**31:
-                packed, self.act_channels = tq_ops.pack_conv_weight(codes[:, :, None, None])
+                packed, self.act_channels, self.engine, self.kc_steps = _pack_termpair(
+                    codes[:, :, None, None], data_bits, weight_bits)
                 self.termpair = True
         else:
             wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
@@ -283,7 +305,7 @@ class TRLinearLayer(nn.Module):
             return self.linear(self.input_quant(x))
         return tq_ops.tr_linear(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, self.linear.bias,
-                                self.linear.out_features)
+                                self.linear.out_features, self.kc_steps)
 
     def tracking(self, tracking):
         if not tracking:

@@ -78,8 +78,31 @@ def test_conv_argument_validation():
 
 def test_act_encode_rejects_wide_codes():
     lib = tq_native.lib()
-    rc = lib.tq_act_encode(None, 1, 1, 8, 2, 2, 1.0, 16, 3, None, 8, None)
+    rc = lib.tq_act_encode(None, 1, 1, 8, 2, 2, 1.0, 16, 3, None, 8, 0, None)
     assert rc == 2 and b"bitwidth" in lib.tq_last_error()
+    # fp16 codes are exact only up to 11 bits
+    rc = lib.tq_act_encode(None, 1, 1, 8, 2, 2, 1.0, 12, 3, None, 8, 1, None)
+    assert rc == 2 and b"fp16" in lib.tq_last_error()
+    rc = lib.tq_act_encode(None, 1, 1, 8, 2, 2, 1.0, 9, 3, None, 8, 7, None)
+    assert rc == 1 and b"format" in lib.tq_last_error()
+
+
+def test_conv_f16_argument_validation():
+    lib = tq_native.lib()
+    # kp must be a multiple of 64 for the MFMA engine
+    rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 4, 3, 3, 160, 1, 1, 1, 1, 1, 1,
+                                    1.0, None, None, 8, 8, 1, 0, None, None)
+    assert rc == 1 and b"64" in lib.tq_last_error()
+    rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 4, 3, 3, 192, 1, 1, 1, 1, 1, 1,
+                                    1.0, None, None, 8, 8, 1, -1, None, None)
+    assert rc == 1 and b"kc_steps" in lib.tq_last_error()
+    epi = tq_native.ConvEpilogue()
+    epi.split_k = 2
+    out = ctypes.c_void_p(16)
+    rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 4, 3, 3, 192, 1, 1, 1, 1, 1, 1,
+                                    1.0, None, out, 8, 8, 1, 0, ctypes.byref(epi), None)
+    assert rc == 2 and b"split" in lib.tq_last_error()
+    assert lib.tq_conv2d_mfma_num_configs() >= 1
 
 
 def test_ops_reject_cpu_tensors_like_the_reference():

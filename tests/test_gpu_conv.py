@@ -30,8 +30,14 @@ def _ref(x, w, bias, sf_x, sf_w, db, dt, wb, g, k, stride, padding, dilation):
     return y, mag, wq
 
 
+@pytest.fixture(params=["mfma", "valu"])
+def engine(request, monkeypatch):
+    monkeypatch.setenv("TQ_CONV_ENGINE", request.param)
+    return request.param
+
+
 def _run(n, c, h, w_, cout, ksz, stride, padding, dilation, bias, channels_last, seed,
-         db=9, dt=3, wb=9, g=8, k=12):
+         db=9, dt=3, wb=9, g=8, k=12, engine=None):
     gen = torch.Generator().manual_seed(seed)
     x = torch.relu(torch.randn(n, c, h, w_, generator=gen))
     w = torch.randn(cout, c, ksz, ksz, generator=gen) * 0.05
@@ -43,6 +49,9 @@ def _run(n, c, h, w_, cout, ksz, stride, padding, dilation, bias, channels_last,
             conv.bias.copy_(b)
     layer = tr_layer.TRConv2dLayer(conv.to(DEV), db, dt, wb, g, k)
     assert layer.termpair
+    if engine is not None:
+        assert layer.engine == engine
+        assert layer.w_codes.dtype == (torch.float16 if engine == "mfma" else torch.int16)
     layer.input_quant.tracking = False
     layer.input_quant.sf = 0.02
     xd = x.to(DEV)
@@ -77,37 +86,102 @@ def _run(n, c, h, w_, cout, ksz, stride, padding, dilation, bias, channels_last,
     (1, 512, 7, 7, 512, 3, 1, 1, 1, False),
 ])
 @pytest.mark.parametrize("channels_last", [False, True])
-def test_termpair_conv_matches_reference(cfg, channels_last):
-    _run(*cfg, channels_last=channels_last, seed=hash(cfg) % 1000)
+def test_termpair_conv_matches_reference(cfg, channels_last, engine):
+    _run(*cfg, channels_last=channels_last, seed=hash(cfg) % 1000, engine=engine)
 
 
-def test_termpair_conv_group_sizes():
+def test_termpair_conv_group_sizes(engine):
     for g, k in [(1, 9), (2, 3), (16, 24), (32, 48)]:
-        _run(2, 64, 8, 8, 64, 3, 1, 1, 1, False, True, seed=g, g=g, k=k)
+        _run(2, 64, 8, 8, 64, 3, 1, 1, 1, False, True, seed=g, g=g, k=k, engine=engine)
 
 
-def test_act_codes_bit_exact():
+@pytest.mark.parametrize("dtype", [torch.int16, torch.float16])
+def test_act_codes_bit_exact(dtype):
+    import tq_native
     torch.manual_seed(9)
     x = torch.randn(2, 40, 6, 5, device=DEV)
     for fmt in (torch.contiguous_format, torch.channels_last):
         xi = x.to(memory_format=fmt)
-        codes = torch.empty((2, 6, 5, 40), dtype=torch.int16, device=DEV)
-        import tq_native
+        codes = torch.empty((2, 6, 5, 40), dtype=dtype, device=DEV)
         nhwc = fmt == torch.channels_last
         tq_native.act_encode(xi, nhwc, 0.01, 9, 3, codes)
         exp = oracle.tr(x.cpu().numpy().reshape(1, -1, 1, 1), 0.01, 9, 1, 3).reshape(x.shape)
         exp_codes = np.rint(exp / np.float32(0.01)).astype(np.int64)
-        assert torch.equal(codes.cpu().long().permute(0, 3, 1, 2),
-                           torch.from_numpy(exp_codes))
+        got = codes.cpu().double()
+        assert torch.equal(got, got.round())  # fp16 codes are exact integers
+        assert torch.equal(got.long().permute(0, 3, 1, 2), torch.from_numpy(exp_codes))
 
 
-def test_termpair_resnet_layer1_full_batch():
+def _engines_pair(cin, cout, ksz, stride, pad, x, db, dt, wb, g, k, sf_x, w=None, seed=0):
+    """The same layer built on both engines, run on x; returns (mfma layer, y_mfma, y_valu)."""
+    import os
+    torch.manual_seed(seed)
+    conv = torch.nn.Conv2d(cin, cout, ksz, stride, pad, bias=True)
+    if w is not None:
+        with torch.no_grad():
+            conv.weight.copy_(w)
+    outs, layers = [], []
+    old = os.environ.get("TQ_CONV_ENGINE")
+    try:
+        for eng in ("mfma", "valu"):
+            os.environ["TQ_CONV_ENGINE"] = eng
+            lay = tr_layer.TRConv2dLayer(copy_conv(conv).to(DEV), db, dt, wb, g, k)
+            assert lay.engine == eng
+            lay.input_quant.tracking = False
+            lay.input_quant.sf = sf_x
+            with torch.no_grad():
+                outs.append(lay(x).cpu())
+            layers.append(lay)
+    finally:
+        if old is None:
+            os.environ.pop("TQ_CONV_ENGINE", None)
+        else:
+            os.environ["TQ_CONV_ENGINE"] = old
+    return layers[0], outs[0], outs[1]
+
+
+def copy_conv(conv):
+    import copy
+    return copy.deepcopy(conv)
+
+
+@pytest.mark.parametrize("layer", [1, 5, 7, 10, 16])
+def test_mfma_engine_bit_identical_to_valu(layer):
+    """Both engines sum the same integers exactly, so outputs match bit for bit (ResNet-18
+    TR layer shapes, odd batch: partial tiles)."""
+    from conftest import RESNET18_TR
+    cin, cout, ksz, s, hin = RESNET18_TR[layer - 1]
+    torch.manual_seed(layer)
+    x = torch.relu(torch.randn(3, cin, hin, hin, device=DEV)).to(
+        memory_format=torch.channels_last)
+    lay, ym, yv = _engines_pair(cin, cout, ksz, s, ksz // 2, x, 9, 3, 9, 8, 12, 0.02,
+                                seed=layer)
+    assert lay.kc_steps >= 0
+    assert torch.equal(ym, yv)
+
+
+def test_mfma_flush_window_exact_at_extremes():
+    """Saturated activations (every code 511) against constant maximal weights (every code
+    256): one K-step of products is 2^23, so the fp32 accumulators must be flushed every 2
+    K-steps; the 4608-deep sums (6.0e8) must still match the VALU engine bit for bit."""
+    cin, cout = 512, 128
+    w = torch.full((cout, cin, 3, 3), 0.01)
+    w[::2] *= -1.0
+    x = torch.full((2, cin, 7, 7), 100.0, device=DEV).to(memory_format=torch.channels_last)
+    lay, ym, yv = _engines_pair(cin, cout, 3, 1, 1, x, 9, 3, 9, 1, 9, 0.02, w=w)
+    assert lay.kc_steps == 2
+    assert torch.equal(ym, yv)
+    assert ym.abs().max().item() > 2**24 * 0.02 * lay.w_sf
+
+
+def test_termpair_resnet_layer1_full_batch(engine):
     """A ResNet-18 layer1 conv at the bench batch (256x64x56x56), checked on 4 images."""
     torch.manual_seed(0)
     conv = torch.nn.Conv2d(64, 64, 3, 1, 1, bias=False)
     torch.nn.init.kaiming_normal_(conv.weight, mode='fan_out', nonlinearity='relu')
     w = conv.weight.detach().clone()
     layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 9, 8, 12)
+    assert layer.engine == engine
     layer.input_quant.tracking = False
     layer.input_quant.sf = 0.01
     x = torch.relu(torch.randn(256, 64, 56, 56, device=DEV)).to(

@@ -32,9 +32,15 @@ def _layer(cin, cout, k, s, seed):
     return layer, bn
 
 
+@pytest.fixture(params=["mfma", "valu"])
+def engine(request, monkeypatch):
+    monkeypatch.setenv("TQ_CONV_ENGINE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("cfg", [(64, 64, 3, 1, 14), (64, 128, 3, 2, 15), (64, 128, 1, 2, 14),
                                  (128, 256, 3, 1, 7)])
-def test_fused_epilogue_matches_reference_composition(cfg):
+def test_fused_epilogue_matches_reference_composition(cfg, engine):
     cin, cout, k, s, hw = cfg
     layer, bn = _layer(cin, cout, k, s, seed=cin + k)
     conv = tq_fuse._Conv(layer, bn)
@@ -43,7 +49,8 @@ def test_fused_epilogue_matches_reference_composition(cfg):
     nxt_conv = tq_fuse._Conv(nxt, None)
     torch.manual_seed(7)
     x = torch.relu(torch.randn(2, cin, hw, hw, device=DEV))
-    codes = torch.empty((2, hw, hw, conv.cp_in), dtype=torch.int16, device=DEV)
+    assert conv.code_dtype == (torch.float16 if engine == "mfma" else torch.int16)
+    codes = torch.empty((2, hw, hw, conv.cp_in), dtype=conv.code_dtype, device=DEV)
     tq_native.act_encode(x.contiguous(memory_format=torch.channels_last), True, 0.03, 9, 3,
                          codes)
     ho, wo = conv.out_hw(hw, hw)
@@ -69,7 +76,7 @@ def test_fused_epilogue_matches_reference_composition(cfg):
     assert torch.equal(got, torch.from_numpy(exp_codes))
 
 
-def test_fused_resnet_matches_module_path():
+def test_fused_resnet_matches_module_path(engine):
     torch.manual_seed(0)
     model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
     settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
@@ -91,10 +98,12 @@ def test_fused_resnet_matches_module_path():
                                          (6, [(1, 1), (1, -1), (5, -1), (4, -1)]),
                                          (16, [(1, 1), (1, -1), (4, -1), (4, 3)]),
                                          (17, [(1, 1), (1, -1), (3, -1)])])
-def test_schedules_are_bit_identical(layer, cfgs):
-    """Data-parallel, K-split (atomics) and stream-K (slab fixup) schedules sum the same
-    integers, so every output and code must be bit-identical."""
+def test_schedules_are_bit_identical(layer, cfgs, monkeypatch):
+    """Data-parallel, K-split (atomics) and stream-K (slab fixup) schedules of the VALU
+    engine and both tile configs of the MFMA engine sum the same integers, so every output
+    and code must be bit-identical."""
     import tq_ops
+    monkeypatch.setenv("TQ_CONV_ENGINE", "valu")
     from conftest import RESNET18_TR
     cin, cout, k, s, hin = RESNET18_TR[layer - 1]
     batch = 37  # odd pixel count: partial last tile
@@ -122,13 +131,31 @@ def test_schedules_are_bit_identical(layer, cfgs):
                                         quant_a=(0.05, 9, 3), workspace=ws, split_k=sp,
                                         config=cfg)
         outs.append((o.cpu(), ca.cpu()))
+    monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
+    lay_m = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    assert lay_m.engine == "mfma" and torch.equal(lay_m.w_codes[:cout, :k * k * cp].float(),
+                                                   lay.w_codes[:cout, :k * k * cp].float())
+    codes_m = torch.empty((batch, hin, hin, cp), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes_m)
+    for cfg in range(1, tq_native.lib().tq_conv2d_mfma_num_configs() + 1):
+        o = torch.full((batch, cout, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.zeros((batch, ho, ho, tq_ops.act_channels(cout)), dtype=torch.float16,
+                         device=DEV)
+        tq_native.conv2d_termpair_fused(codes_m, lay_m.w_codes, cout, k, k, (s, s),
+                                        (k // 2, k // 2), (1, 1), ho, ho, out=o, ch_scale=sc,
+                                        ch_shift=sh, relu=True, codes_a=ca,
+                                        quant_a=(0.05, 9, 3), config=cfg,
+                                        kc_steps=lay_m.kc_steps)
+        outs.append((o.cpu(), ca.cpu().to(torch.int16)))
     o0, c0 = outs[0]
     assert not torch.isnan(o0).any()
     for o, c in outs[1:]:
         assert torch.equal(o, o0) and torch.equal(c, c0)
 
 
-def test_stem_bn_relu_maxpool_encode():
+@pytest.mark.parametrize("dtype", [torch.int16, torch.float16])
+def test_stem_bn_relu_maxpool_encode(dtype):
     torch.manual_seed(11)
     bn = nn.BatchNorm2d(64).to(DEV).eval()
     with torch.no_grad():
@@ -142,7 +169,7 @@ def test_stem_bn_relu_maxpool_encode():
     sc = a.float().contiguous()
     sh = (bn.bias.double() - bn.running_mean.double() * a).float().contiguous()
     out = torch.empty_like(ref, memory_format=torch.channels_last)
-    codes = torch.empty((3, ref.shape[2], ref.shape[3], 64), dtype=torch.int16, device=DEV)
+    codes = torch.empty((3, ref.shape[2], ref.shape[3], 64), dtype=dtype, device=DEV)
     tq_native.bn_relu_maxpool_encode(x, sc, sh, 3, 2, 1, out, codes_a=codes,
                                      quant_a=(0.05, 9, 3))
     assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)

@@ -150,14 +150,30 @@ def test_trconv_layer_weight_is_reference_tr(oracle_tr):
     assert layer.w_sf == sf
     assert torch.equal(layer.conv.weight.detach(), torch.from_numpy(oracle.tr(w.numpy(), sf, 9,
                                                                               8, 12)))
-    assert layer.termpair and layer.w_codes.dtype == torch.int16
-    assert layer.w_codes.shape[1] % 32 == 0 and layer.w_codes.shape[0] % 128 == 0
+    # 9-bit codes are exact fp16 values: the MFMA engine (fp16 codes, Kp % 64 == 0)
+    assert layer.termpair and layer.engine == "mfma"
+    assert layer.w_codes.dtype == torch.float16 and layer.kc_steps == 0
+    assert layer.w_codes.shape[1] % 64 == 0 and layer.w_codes.shape[0] % 128 == 0
     # packed codes reproduce the fake-quantized weights: [O][kh][kw][c] order
     packed = layer.w_codes[:8, :9 * 16].view(8, 3, 3, 16).permute(0, 3, 1, 2).float()
     assert torch.equal(packed * np.float32(sf), layer.conv.weight.detach())
     for attr in ("conv", "input_quant", "w_sf", "group_size", "num_terms", "weight_bits",
                  "data_bits", "data_terms"):
         assert hasattr(layer, attr)
+
+
+def test_trconv_layer_engine_choice(oracle_tr, monkeypatch):
+    torch.manual_seed(2)
+    conv = nn.Conv2d(16, 8, 3, padding=1)
+    lay = tr_layer.TRConv2dLayer(conv, 12, 3, 9, 8, 12)  # 12-bit activations: not fp16-exact
+    assert lay.engine == "valu" and lay.w_codes.dtype == torch.int16
+    assert lay.w_codes.shape[1] % 32 == 0
+    monkeypatch.setenv("TQ_CONV_ENGINE", "valu")
+    lay = tr_layer.TRConv2dLayer(nn.Conv2d(16, 8, 3, padding=1), 9, 3, 9, 8, 12)
+    assert lay.engine == "valu"
+    monkeypatch.setenv("TQ_CONV_ENGINE", "bogus")
+    with pytest.raises(RuntimeError, match="TQ_CONV_ENGINE"):
+        tr_layer.TRConv2dLayer(nn.Conv2d(16, 8, 3, padding=1), 9, 3, 9, 8, 12)
 
 
 def test_tracking_histogram_and_passthrough(stub_tr):
@@ -248,3 +264,15 @@ def test_lstm_counts_match_published(stub_tr):
         q = evaluate_lstm.convert_model(model, st, 8, 8)
         tmacs, _ = profile_model.get_model_ops(q, inputs)
         assert tmacs == pub_t["tmacs"][i]
+
+
+def test_mfma_flush_steps_bounds():
+    import tq_ops  # noqa: F811
+    codes = torch.full((4, 64, 3, 3), 256, dtype=torch.int32)
+    packed, _ = tq_ops.pack_conv_weight(codes, "mfma")
+    assert tq_ops.mfma_flush_steps(packed, 9) == 2
+    assert tq_ops.mfma_flush_steps(packed, 8) == 4
+    assert tq_ops.mfma_flush_steps(packed, 11) == -1
+    small = torch.ones((4, 64, 3, 3), dtype=torch.int32)
+    packed, _ = tq_ops.pack_conv_weight(small, "mfma")
+    assert tq_ops.mfma_flush_steps(packed, 9) == 0

@@ -34,7 +34,7 @@ def main():
     cp = tq_ops.act_channels(cin)
     xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
         memory_format=torch.channels_last)
-    codes = torch.empty((args.batch, hin, hin, cp), dtype=torch.int16, device=dev)
+    codes = torch.empty((args.batch, hin, hin, cp), dtype=layer.w_codes.dtype, device=dev)
     tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
     ho = (hin + 2 * (k // 2) - k) // s + 1
     o = torch.empty((args.batch, cout, ho, ho), device=dev, memory_format=torch.channels_last)
@@ -43,7 +43,8 @@ def main():
     sh = torch.zeros(cout, dtype=torch.float64, device=dev)
     fn = lambda: tq_native.conv2d_termpair_fused(
         codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho, out=o,
-        ch_scale=sc, ch_shift=sh, workspace=ws, split_k=args.split, config=args.config)
+        ch_scale=sc, ch_shift=sh, workspace=None if layer.engine == "mfma" else ws,
+        split_k=args.split, config=args.config, kc_steps=layer.kc_steps)
     t = time_fn(fn, args.iters)
     mac = args.batch * cout * ho * ho * cin * k * k
     print("layer %d cfg %d split %d: %.1f us  %.1f TMAC/s" % (args.layer, args.config,

@@ -43,9 +43,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--engine", choices=("mfma", "valu"), default="mfma")
     ap.add_argument("--sweep", action="store_true",
                     help="time every tile config x K-split per layer (fused NHWC entry)")
     args = ap.parse_args()
+    os.environ["TQ_CONV_ENGINE"] = args.engine
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
 
@@ -76,18 +78,19 @@ def main():
             memory_format=torch.channels_last)
         ho = (hin + 2 * (k // 2) - k) // s + 1
         cp = tq_ops.act_channels(cin)
-        codes = torch.empty((args.batch, hin, hin, cp), dtype=torch.int16, device=dev)
+        codes = torch.empty((args.batch, hin, hin, cp), dtype=layer.w_codes.dtype, device=dev)
         tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
         o = torch.empty((args.batch, cout, ho, ho), device=dev,
                         memory_format=torch.channels_last)
         fn = lambda: tq_native.conv2d_termpair(codes, layer.w_codes, cout, k, k, (s, s),
-                                               (k // 2, k // 2), (1, 1), 1e-4, None, o, True)
+                                               (k // 2, k // 2), (1, 1), 1e-4, None, o, True,
+                                               layer.kc_steps)
         t = time_fn(fn, args.iters)
         mac = args.batch * cout * ho * ho * cin * k * k
         total_mac += mac
         total_t += t
-        print("conv%02d %3d->%3d k%d s%d %2dx%2d: %8.1f us  %6.1f TMAC/s" % (
-            i + 1, cin, cout, k, s, hin, hin, t * 1e6, mac / t / 1e12))
+        print("conv%02d %3d->%3d k%d s%d %2dx%2d: %8.1f us  %6.1f TMAC/s  kc=%d" % (
+            i + 1, cin, cout, k, s, hin, hin, t * 1e6, mac / t / 1e12, layer.kc_steps))
     print("conv total: %.2f ms  %.1f TMAC/s  -> %.0f img/s (convs only)" % (
         total_t * 1e3, total_mac / total_t / 1e12, args.batch / total_t))
     if args.sweep:
@@ -95,7 +98,9 @@ def main():
 
 
 def sweep(args, dev):
-    ncfg = tq_native.lib().tq_conv2d_num_configs()
+    mfma = args.engine == "mfma"
+    ncfg = (tq_native.lib().tq_conv2d_mfma_num_configs() if mfma else
+            tq_native.lib().tq_conv2d_num_configs())
     best_total = 0.0
     auto_total = 0.0
     seen = {}
@@ -110,7 +115,7 @@ def sweep(args, dev):
         cp = tq_ops.act_channels(cin)
         xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
             memory_format=torch.channels_last)
-        codes = torch.empty((args.batch, hin, hin, cp), dtype=torch.int16, device=dev)
+        codes = torch.empty((args.batch, hin, hin, cp), dtype=layer.w_codes.dtype, device=dev)
         tq_native.act_encode(xi, True, 0.02, 9, 3, codes)
         ho = (hin + 2 * (k // 2) - k) // s + 1
         o = torch.empty((args.batch, cout, ho, ho), device=dev,
@@ -121,10 +126,11 @@ def sweep(args, dev):
         mac = args.batch * cout * ho * ho * cin * k * k
         res = {}
         for cfg in range(0, ncfg + 1):
-            for sp in ([1, -1, 3] if cfg else [0]):
+            for sp in ([1, -1, 3] if cfg and not mfma else [0]):
                 fn = lambda: tq_native.conv2d_termpair_fused(
                     codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho,
-                    out=o, ch_scale=sc, ch_shift=sh, workspace=ws, split_k=sp, config=cfg)
+                    out=o, ch_scale=sc, ch_shift=sh, workspace=None if mfma else ws,
+                    split_k=sp, config=cfg, kc_steps=layer.kc_steps)
                 res[(cfg, sp)] = time_fn(fn, max(5, args.iters // 2))
         best = min(res, key=res.get)
         auto = res[(0, 0)]
