@@ -37,6 +37,9 @@ namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float float16v __attribute__((ext_vector_type(16)));
+// Native vector (not HIP's union-based uint4, which defeats SROA: arrays of it become
+// allocas that the backend promotes to LDS).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kKStep = 64;  // codes per K-step
 
@@ -46,8 +49,8 @@ __device__ __forceinline__ int swz(int row, int chunk) {
 
 template <int BM, int BN>
 struct MfmaSmem {
-  uint4 As[2][BM * 8];
-  uint4 Bs[2][BN * 8];
+  u32x4 As[2][BM * 8];
+  u32x4 Bs[2][BN * 8];
 };
 
 // Accumulator state of one wave: 2 x 2 blocks of 32 x 32, fp32 (exact window) + int32.
@@ -137,49 +140,55 @@ __device__ __forceinline__ void mfma_mainloop(const ConvArgs& a, int m0, int64_t
   const int ntaps = a.KH * a.KW;
   const int nsteps = k_end - k_begin;
 
-  uint4 ra[A_ROWS], rb[B_ROWS];
-  auto load_tile = [&](int step) {
-#pragma unroll
-    for (int r = 0; r < A_ROWS; ++r)
-      ra[r] = *reinterpret_cast<const uint4*>(wrow[r] + (int64_t)step * kKStep);
-#pragma unroll
-    for (int r = 0; r < B_ROWS; ++r) {
-      rb[r] = make_uint4(0, 0, 0, 0);
-      if (ktap < ntaps) {
-        const int ih = ih0[r] + kr * a.dh;
-        const int iw = iw0[r] + ks * a.dw;
-        if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-          rb[r] = *reinterpret_cast<const uint4*>(xg + ((pbase[r] + ih) * a.W + iw) * a.Cp + kc);
-      }
-    }
-    kc += kKStep;
-    while (kc >= a.Cp) {
-      kc -= a.Cp;
-      ++ktap;
-      if (++ks == a.KW) {
-        ks = 0;
-        ++kr;
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < A_ROWS; ++r) sm.As[buf][swz(r0 + 32 * r, ch)] = ra[r];
-#pragma unroll
-    for (int r = 0; r < B_ROWS; ++r) sm.Bs[buf][swz(r0 + 32 * r, ch)] = rb[r];
-  };
-
   if (nsteps <= 0) return;
   const int r32 = lane & 31;
   const int hh = lane >> 5;
   const int kc_steps = a.kc_steps > 0 ? a.kc_steps : (1 << 30);
   int since_flush = 0;
-  load_tile(0);
-  store_tile(0);
+
+  // Global -> registers of one K-step.
+  // Out-of-range taps load from the (valid) tensor base and are zeroed when stored to LDS
+  // (a select at load time would make the wave wait for the load right there).
+  u32x4 ra[A_ROWS], rb[B_ROWS];
+  uint32_t okmask = 0;
+#define TQ_LOAD_STEP(step)                                                                  \
+  {                                                                                         \
+    _Pragma("unroll") for (int r = 0; r < A_ROWS; ++r) ra[r] =                              \
+        *reinterpret_cast<const u32x4*>(wrow[r] + (int64_t)(step) * kKStep);                \
+    okmask = 0;                                                                             \
+    _Pragma("unroll") for (int r = 0; r < B_ROWS; ++r) {                                    \
+      const int ih = ih0[r] + kr * a.dh;                                                    \
+      const int iw = iw0[r] + ks * a.dw;                                                    \
+      const bool ok = ktap < ntaps && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;           \
+      const uint16_t* src = ok ? xg + ((pbase[r] + ih) * a.W + iw) * a.Cp + kc : xg;         \
+      rb[r] = *reinterpret_cast<const u32x4*>(src);                                          \
+      okmask |= (uint32_t)ok << r;                                                          \
+    }                                                                                       \
+    kc += kKStep;                                                                           \
+    while (kc >= a.Cp) {                                                                    \
+      kc -= a.Cp;                                                                           \
+      ++ktap;                                                                               \
+      if (++ks == a.KW) {                                                                   \
+        ks = 0;                                                                             \
+        ++kr;                                                                               \
+      }                                                                                     \
+    }                                                                                       \
+  }
+#define TQ_STORE_STEP(buf)                                                                  \
+  {                                                                                         \
+    _Pragma("unroll") for (int r = 0; r < A_ROWS; ++r) sm.As[buf][swz(r0 + 32 * r, ch)] =   \
+        ra[r];                                                                              \
+    _Pragma("unroll") for (int r = 0; r < B_ROWS; ++r) sm.Bs[buf][swz(r0 + 32 * r, ch)] =   \
+        ((okmask >> r) & 1u) ? rb[r] : (u32x4)0u;                                           \
+  }
+
+  TQ_LOAD_STEP(0)
+  TQ_STORE_STEP(0)
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    if (step + 1 < nsteps) load_tile(step + 1);
+    const bool more = step + 1 < nsteps;
+    if (more) TQ_LOAD_STEP(step + 1)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int c = 2 * s + hh;
@@ -200,9 +209,11 @@ __device__ __forceinline__ void mfma_mainloop(const ConvArgs& a, int m0, int64_t
       acc_flush(acc);
       since_flush = 0;
     }
-    if (step + 1 < nsteps) store_tile(cur ^ 1);
+    if (more) TQ_STORE_STEP(cur ^ 1)
     __syncthreads();
   }
+#undef TQ_LOAD_STEP
+#undef TQ_STORE_STEP
   acc_flush(acc);
 }
 
