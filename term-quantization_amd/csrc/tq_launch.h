@@ -40,6 +40,9 @@ struct ConvArgs {
   // K-steps of 64 codes, a window whose |partial sums| the host has bounded by 2^24 (so
   // every fp32 partial sum is an exact integer); 0 = never needed.
   int kc_steps;
+  // MFMA patch engine (set by its launcher): patch slot pixels and number of patch buffers
+  int patch_px, patch_bufs;
+  int m_slow;  // MFMA engines: 1 = Cout tile is the slow index of the tile order
   // Execution choices: config 0 = heuristic, 1..conv_num_configs() = a fixed tile config;
   // splits: 1 data-parallel, > 1 K-split with int32 atomics into ws ([P][Cout]), -1
   // stream-K (ws holds two BM x BN int32 slabs per resident block); NHWC output only.
@@ -91,5 +94,8 @@ hipError_t launch_conv2d_tp(const ConvArgs& a, int out_nhwc, hipStream_t stream)
 // MFMA engine: x, w hold fp16 codes (kCodesF16), Kp % 64 == 0, Cout_pad % 128 == 0.
 hipError_t launch_conv2d_mfma(const ConvArgs& a, int out_nhwc, hipStream_t stream);
 int conv_mfma_num_configs();
+// MFMA input-patch engine (tr_conv_patch.hip): stride-1 convs with Cp % 64 == 0, NHWC out.
+bool conv_patch_eligible(const ConvArgs& a, int out_nhwc);
+hipError_t launch_conv2d_patch(const ConvArgs& a, int mb, hipStream_t stream);
 
 }  // namespace tq

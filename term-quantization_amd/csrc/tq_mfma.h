@@ -1,0 +1,96 @@
+// MFMA-engine building blocks shared by the term-pair conv kernels on the matrix cores
+// (tr_conv_mfma.hip: gather engines; tr_conv_patch.hip: input-patch engine).  The exactness
+// argument for fp16 term-sum codes on v_mfma_f32_32x32x16_f16 is in tr_conv_mfma.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tq {
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float float16v __attribute__((ext_vector_type(16)));
+// Native vector (not HIP's union-based uint4, which defeats SROA: arrays of it become
+// allocas that the backend promotes to LDS).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kKStep = 64;  // codes per K-step
+
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * 8 + (chunk ^ ((row >> 1) & 7));
+}
+
+// Accumulator state of one wave: MB x 2 blocks of 32 x 32, fp32 (exact window) + int32.
+template <int MB>
+struct MfmaAcc {
+  float16v f[MB][2];
+  int i[MB][2][16];
+};
+
+template <int MB>
+__device__ __forceinline__ void acc_zero(MfmaAcc<MB>& acc) {
+#pragma unroll
+  for (int bm = 0; bm < MB; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc.f[bm][bn][r] = 0.0f;
+        acc.i[bm][bn][r] = 0;
+      }
+    }
+}
+
+// fp32 partial sums are exact integers below 2^24: move them into the int32 sums.
+template <int MB>
+__device__ __forceinline__ void acc_flush(MfmaAcc<MB>& acc) {
+#pragma unroll
+  for (int bm = 0; bm < MB; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc.i[bm][bn][r] += (int)acc.f[bm][bn][r];
+        acc.f[bm][bn][r] = 0.0f;
+      }
+    }
+}
+
+// LDS staging by global_load_lds_dwordx4 (LDS-DMA: no VGPR destination; the LDS image of
+// one wave-instruction is lane-linear, base + lane * 16).
+__device__ u32x4 g_zero_page[64];  // static storage: all zeros, never written
+
+__device__ __forceinline__ void glds16(const void* src, u32x4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 |
+// vmcnt[5:4] << 14), other counters untouched.
+#define TQ_WAIT_VM(n) \
+  __builtin_amdgcn_s_waitcnt(((n) & 15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14))
+
+// s_waitcnt vmcnt(n) for a runtime n: counts above 15 wait for 15 (stricter, still correct).
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  switch (n) {
+    case 0: TQ_WAIT_VM(0); break;
+    case 1: TQ_WAIT_VM(1); break;
+    case 2: TQ_WAIT_VM(2); break;
+    case 3: TQ_WAIT_VM(3); break;
+    case 4: TQ_WAIT_VM(4); break;
+    case 5: TQ_WAIT_VM(5); break;
+    case 6: TQ_WAIT_VM(6); break;
+    case 7: TQ_WAIT_VM(7); break;
+    case 8: TQ_WAIT_VM(8); break;
+    case 9: TQ_WAIT_VM(9); break;
+    case 10: TQ_WAIT_VM(10); break;
+    case 11: TQ_WAIT_VM(11); break;
+    case 12: TQ_WAIT_VM(12); break;
+    case 13: TQ_WAIT_VM(13); break;
+    case 14: TQ_WAIT_VM(14); break;
+    default: TQ_WAIT_VM(15); break;
+  }
+}
+
+}  // namespace
+}  // namespace tq

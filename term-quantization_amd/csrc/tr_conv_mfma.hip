@@ -27,25 +27,16 @@
 // are 8 chunks of 16 B with chunk' = chunk ^ ((row >> 1) & 7): the MFMA fragment reads (32
 // rows at one chunk per half-wave) and the staging writes (2 rows x 8 chunks per 16 lanes)
 // are both bank-conflict free.
+#include <stdlib.h>
+
 #include "tq_device.h"
 #include "tq_epilogue.h"
 #include "tq_launch.h"
+#include "tq_mfma.h"
 
 namespace tq {
 
 namespace {
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float float16v __attribute__((ext_vector_type(16)));
-// Native vector (not HIP's union-based uint4, which defeats SROA: arrays of it become
-// allocas that the backend promotes to LDS).
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kKStep = 64;  // codes per K-step
-
-__device__ __forceinline__ int swz(int row, int chunk) {
-  return row * 8 + (chunk ^ ((row >> 1) & 7));
-}
 
 template <int BM, int BN>
 struct MfmaSmem {
@@ -53,43 +44,10 @@ struct MfmaSmem {
   u32x4 Bs[2][BN * 8];
 };
 
-// Accumulator state of one wave: 2 x 2 blocks of 32 x 32, fp32 (exact window) + int32.
-struct MfmaAcc {
-  float16v f[2][2];
-  int i[2][2][16];
-};
-
-__device__ __forceinline__ void acc_zero(MfmaAcc& acc) {
-#pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-    for (int bn = 0; bn < 2; ++bn) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc.f[bm][bn][r] = 0.0f;
-        acc.i[bm][bn][r] = 0;
-      }
-    }
-}
-
-// fp32 partial sums are exact integers below 2^24: move them into the int32 sums.
-__device__ __forceinline__ void acc_flush(MfmaAcc& acc) {
-#pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-    for (int bn = 0; bn < 2; ++bn) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc.i[bm][bn][r] += (int)acc.f[bm][bn][r];
-        acc.f[bm][bn][r] = 0.0f;
-      }
-    }
-}
-
 // K-steps [k_begin, k_end) of block tile (m0, n0) into acc.  Ends on a barrier.
 template <int BM, int BN>
 __device__ __forceinline__ void mfma_mainloop(const ConvArgs& a, int m0, int64_t n0,
-                                              int k_begin, int k_end, MfmaAcc& acc,
+                                              int k_begin, int k_end, MfmaAcc<2>& acc,
                                               MfmaSmem<BM, BN>& sm) {
   constexpr int WN = BN / 64;  // waves along N
   constexpr int A_ROWS = BM / 32;
@@ -221,7 +179,7 @@ __device__ __forceinline__ void mfma_mainloop(const ConvArgs& a, int m0, int64_t
 // 8*(reg>>2) + 4*hh + (reg&3), i.e. 4 consecutive channels per register quad.
 template <int BM, int BN, bool OUT_NHWC>
 __device__ __forceinline__ void mfma_epilogue(const ConvArgs& a, int m0, int64_t n0,
-                                              const MfmaAcc& acc) {
+                                              const MfmaAcc<2>& acc) {
   constexpr int WN = BN / 64;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -279,10 +237,213 @@ __global__ __launch_bounds__(256, 2) void conv2d_tp_mfma_kernel(ConvArgs a) {
   const int mt = (a.Cout + BM - 1) / BM;
   const int m0 = (tile % mt) * BM;
   const int64_t n0 = (int64_t)(tile / mt) * BN;
-  MfmaAcc acc;
+  MfmaAcc<2> acc;
   acc_zero(acc);
   mfma_mainloop<BM, BN>(a, m0, n0, 0, a.Kp / kKStep, acc, sm);
   mfma_epilogue<BM, BN, OUT_NHWC>(a, m0, n0, acc);
+}
+
+// ---------------------------------------------------------------------------------------
+// Pipelined engine (Cp % 64 == 0: every K-step lies inside one filter tap).  Operands go
+// global -> LDS directly (global_load_lds_dwordx4, no staging registers) into an NS-deep
+// ring of K-step images; stage s+NS-1 is issued while stage s is multiplied, retired by a
+// counted vmcnt + raw s_barrier (never a vmcnt(0) inside the loop).  The LDS image of a
+// wave-instruction is lane-linear (base + lane*16), so the bank swizzle moves to the SOURCE:
+// lane l fills slot (l & 7) of row r with logical chunk (l & 7) ^ ((r >> 1) & 7), and the
+// fragment reads apply the same involution (swz).  Out-of-range taps and pixels read a
+// zero page.  The epilogue transposes each wave's 64 x 64 int32 tile through the freed LDS
+// ring so every store instruction writes whole 256-byte pixel rows (channels_last).
+constexpr int pipe_threads(int bm, int bn) { return (bm / 64) * (bn / 64) * 64; }
+
+template <int BM, int BN, int NS>
+struct PipeCfg {
+  static constexpr int WAVES = (BM / 64) * (BN / 64);
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int WN = BN / 64;
+  static constexpr int STAGE = (BM + BN) * 8;  // u32x4 per K-step image
+  static constexpr int AI = BM / 8 / WAVES;    // A wave-instructions per wave and stage
+  static constexpr int BI = BN / 8 / WAVES;    // B wave-instructions per wave and stage
+  static constexpr int LPW = AI + BI;          // vmcnt units per wave and stage
+  static constexpr int LDS = NS * STAGE > WAVES * 1024 ? NS * STAGE : WAVES * 1024;
+  static_assert(AI >= 1 && BI >= 1 && AI * WAVES * 8 == BM && BI * WAVES * 8 == BN, "rows");
+  static_assert(LPW * (NS - 2) <= 63, "vmcnt range");
+};
+
+template <int BM, int BN, int NS, bool OUT_NHWC>
+__global__ __launch_bounds__(pipe_threads(BM, BN), 1) void conv2d_tp_mfma_pipe_kernel(
+    ConvArgs a) {
+  using C = PipeCfg<BM, BN, NS>;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int64_t ntn = (a.P + BN - 1) / BN;
+  const int m0 = (int)(a.m_slow ? tile / ntn : tile % mt) * BM;
+  const int64_t n0 = (a.m_slow ? tile % ntn : tile / mt) * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave / C::WN) * 64;
+  const int wn = (wave % C::WN) * 64;
+  const int lrow = lane >> 3;  // row within a wave-instruction's 8 rows
+  const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
+  const uint16_t* __restrict__ wg = reinterpret_cast<const uint16_t*>(a.w);
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page) + lane * 8;
+
+  // A rows (weights): fixed pointers, advanced by 64 codes per K-step.
+  const uint16_t* arow[C::AI];
+#pragma unroll
+  for (int i = 0; i < C::AI; ++i) {
+    const int r = (wave * C::AI + i) * 8 + lrow;
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    arow[i] = wg + (int64_t)(m0 + r) * a.Kp + c * 8;
+  }
+  // B rows (output pixels): element offset of this lane's chunk at the pixel's input
+  // origin, and a bit mask of the filter taps that fall inside the input (KH*KW <= 64).
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  int64_t boff[C::BI];
+  uint64_t tapmask[C::BI];
+#pragma unroll
+  for (int i = 0; i < C::BI; ++i) {
+    const int r = (wave * C::BI + i) * 8 + lrow;  // B row = pixel n0 + r
+    const int chk = ((lane & 7) ^ (((BM + r) >> 1) & 7)) * 8;
+    const int64_t p = n0 + r;
+    boff[i] = 0;
+    tapmask[i] = 0;
+    if (p < a.P) {
+      const int64_t img = p / HoWo;
+      const int64_t rem = p - img * HoWo;
+      const int oh = (int)(rem / a.Wo);
+      const int ow = (int)(rem - (int64_t)oh * a.Wo);
+      const int ih0 = oh * a.sh - a.ph;
+      const int iw0 = ow * a.sw - a.pw;
+      boff[i] = ((img * a.H + ih0) * a.W + iw0) * a.Cp + chk;
+      for (int kr = 0; kr < a.KH; ++kr) {
+        const int ih = ih0 + kr * a.dh;
+        if (ih < 0 || ih >= a.H) continue;
+        for (int ks = 0; ks < a.KW; ++ks) {
+          const int iw = iw0 + ks * a.dw;
+          if (iw >= 0 && iw < a.W) tapmask[i] |= 1ull << (kr * a.KW + ks);
+        }
+      }
+    }
+  }
+  const int nsteps = a.Kp / kKStep;
+
+  // Issue K-step `st` into ring slot `slot`.  Cp % 64 == 0, so the step lies in one tap:
+  // the tap and its element offset are wave-uniform (scalar) values.
+  auto issue = [&](int st, int slot) {
+    u32x4* img = lds + slot * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::AI; ++i)
+      glds16(arow[i] + (int64_t)st * kKStep, img + (wave * C::AI + i) * 64);
+    const int k0 = st * kKStep;
+    const int tap = k0 / a.Cp;
+    const int cb = k0 - tap * a.Cp;
+    const int kr = tap / a.KW;
+    const int ks = tap - kr * a.KW;
+    const int64_t toff = ((int64_t)kr * a.dh * a.W + (int64_t)ks * a.dw) * a.Cp + cb;
+#pragma unroll
+    for (int i = 0; i < C::BI; ++i) {
+      const bool ok = (tapmask[i] >> tap) & 1ull;  // tap >= KH*KW (K padding): bit clear
+      const uint16_t* src = ok ? xg + (boff[i] + toff) : zero;
+      glds16(src, img + BM * 8 + (wave * C::BI + i) * 64);
+    }
+  };
+
+  MfmaAcc<2> acc;
+  acc_zero(acc);
+  const int r32 = lane & 31;
+  const int hh = lane >> 5;
+  const int kc_steps = a.kc_steps > 0 ? a.kc_steps : (1 << 30);
+  int since_flush = 0;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nsteps) issue(s, s);
+  for (int s = 0; s < nsteps; ++s) {
+    // retire stage s, leaving min(nsteps - 1 - s, NS - 2) later stages in flight
+    const int ahead = min(nsteps - 1 - s, NS - 2);
+    if (ahead >= 2) TQ_WAIT_VM(2 * C::LPW);
+    else if (ahead == 1) TQ_WAIT_VM(C::LPW);
+    else TQ_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();
+    if (s + NS - 1 < nsteps) issue(s + NS - 1, (s + NS - 1) % NS);
+    const u32x4* img = lds + (s % NS) * C::STAGE;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 2 * k + hh;
+      half8 af[2], bf[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        af[b] = __builtin_bit_cast(half8, img[swz(wm + 32 * b + r32, c)]);
+        bf[b] = __builtin_bit_cast(half8, img[swz(BM + wn + 32 * b + r32, c)]);
+      }
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          acc.f[bm][bn] =
+              __builtin_amdgcn_mfma_f32_32x32x16_f16(af[bm], bf[bn], acc.f[bm][bn], 0, 0, 0);
+    }
+    if (++since_flush == kc_steps) {
+      acc_flush(acc);
+      since_flush = 0;
+    }
+  }
+  acc_flush(acc);
+
+  if (!OUT_NHWC) {
+    mfma_epilogue<BM, BN, false>(a, m0, n0, acc);  // NCHW: lanes along pixels already
+    return;
+  }
+  // Transpose each wave's 64 (Cout) x 64 (pixel) int32 tile through LDS:
+  // [pixel][16 slots of 4 channels], slot ^= pixel & 15 (conflict-free both ways).
+  __syncthreads();  // every wave is done with the ring
+  u32x4* t = lds + wave * 1024;
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int px = 32 * bn + r32;
+        const int slot = 8 * bm + 2 * q + hh;
+        u32x4 v;
+        v.x = (uint32_t)acc.i[bm][bn][4 * q];
+        v.y = (uint32_t)acc.i[bm][bn][4 * q + 1];
+        v.z = (uint32_t)acc.i[bm][bn][4 * q + 2];
+        v.w = (uint32_t)acc.i[bm][bn][4 * q + 3];
+        t[px * 16 + (slot ^ (px & 15))] = v;
+      }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
+  __builtin_amdgcn_wave_barrier();
+  const bool vec = (a.Cout & 3) == 0;
+  const int slot = lane & 15;
+  const int co = m0 + wm + 4 * slot;
+  if (co < a.Cout) {
+    double sc[4], sh[4];
+    load_coef(a, co, sc, sh);
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int px = it * 4 + (lane >> 4);
+      const int64_t p = n0 + wn + px;
+      if (p >= a.P) continue;
+      const u32x4 v = t[px * 16 + (slot ^ (px & 15))];
+      const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      emit4_nhwc(a, p, co, acc4, sc, sh, vec);
+    }
+  }
+}
+
+template <int BM, int BN, int NS>
+hipError_t launch_pipe_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) {
+  using C = PipeCfg<BM, BN, NS>;
+  const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + BM - 1) / BM);
+  const dim3 grid((unsigned)tiles);
+  if (out_nhwc)
+    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true><<<grid, C::THREADS, 0, stream>>>(a);
+  else
+    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, false><<<grid, C::THREADS, 0, stream>>>(a);
+  return hipGetLastError();
 }
 
 template <int BM, int BN>
@@ -298,14 +459,37 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 
 }  // namespace
 
-int conv_mfma_num_configs() { return 2; }
+// Configs (1-based through ConvArgs.config): 1-2 register-staged (any Cp), 3-6 pipelined
+// gather (Cp % 64 == 0 and KH*KW <= 64; else 1/2), 7-8 input patch (tr_conv_patch.hip:
+// stride 1, KH*KW >= 2, NHWC out; else the gather default).
+int conv_mfma_num_configs() { return 8; }
 
-hipError_t launch_conv2d_mfma(const ConvArgs& a, int out_nhwc, hipStream_t stream) {
-  if (a.P == 0 || a.Cout == 0) return hipSuccess;
-  int cfg = a.config > 0 ? a.config - 1 : (a.Cout <= 64 ? 1 : 0);
+hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
+  if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
+  ConvArgs a = a_in;
+  // Tile order: with the Cout tile as the slow index, an XCD's contiguous run of tiles
+  // shares one weight slice in its L2 (speed only).  TQ_MSLOW=0/1 overrides (A/B).
+  static const char* ms = getenv("TQ_MSLOW");
+  a.m_slow = ms ? atoi(ms) : 0;
+  const bool pipe_ok = a.Cp % kKStep == 0 && a.KH * a.KW <= 64;
+  int cfg = a.config > 0 ? a.config - 1 : -1;
+  if (cfg >= 6 || cfg < 0) {
+    if (conv_patch_eligible(a, out_nhwc)) {
+      const int mb = cfg == 6 ? 2 : cfg == 7 ? 1 : (a.Cout <= 64 ? 1 : 2);
+      return launch_conv2d_patch(a, mb, stream);
+    }
+    cfg = -1;
+  }
+  // measured (tools/microbench.py --sweep): 64 x 512 (8 waves) for Cout <= 64, else 128 x 256
+  if (cfg < 0) cfg = pipe_ok ? (a.Cout <= 64 ? 5 : 2) : (a.Cout <= 64 ? 1 : 0);
+  if (cfg >= 2 && !pipe_ok) cfg = a.Cout <= 64 ? 1 : 0;
   switch (cfg) {
     case 0: return launch_mfma_cfg<128, 128>(a, out_nhwc, stream);
-    default: return launch_mfma_cfg<64, 256>(a, out_nhwc, stream);
+    case 1: return launch_mfma_cfg<64, 256>(a, out_nhwc, stream);
+    case 2: return launch_pipe_cfg<128, 256, 3>(a, out_nhwc, stream);
+    case 3: return launch_pipe_cfg<64, 256, 3>(a, out_nhwc, stream);
+    case 4: return launch_pipe_cfg<128, 128, 3>(a, out_nhwc, stream);
+    default: return launch_pipe_cfg<64, 512, 2>(a, out_nhwc, stream);
   }
 }
 

@@ -1,0 +1,401 @@
+// Term-pair Conv2d on the matrix cores, input-patch engine (stride-1 convs with KH*KW >= 2
+// and Cp % 64 == 0: every 3x3 conv of ResNet-18 but layer2/3/4.0.conv1).
+//
+// Same arithmetic and exactness argument as tr_conv_mfma.hip (fp16 term-sum codes,
+// v_mfma_f32_32x32x16_f16, fp32 windows of kc_steps K-steps flushed into int32 sums), but
+// the activation operand is not re-gathered per filter tap.  A tile is 256 consecutive
+// output pixels (raster order, may span output rows and images); the input rows those
+// pixels need -- one contiguous run of NHWC pixels -- are staged once per 64-channel chunk
+// as an LDS "patch", and the KH*KW taps of that chunk read their B fragments straight out
+// of it (pixel (oy, ox) at tap (r, q) = patch pixel (oy + r*dh, ox + q*dw) relative to the
+// patch origin; taps that fall into the zero padding read a zero row).  Activation bytes
+// per tile drop from KH*KW * 256 rows to ~(rows spanned + KH - 1) * W rows per chunk.
+//
+// K order: chunk-major, tap-minor: step (c, t) multiplies weight codes
+// w[m][t*Cp + 64c .. +64] by the patch of chunk c shifted by tap t.  The weight K-step
+// images stream through a 3-5 deep LDS ring; the patch of chunk c+1 is issued at the first
+// tap of chunk c into the other patch buffer.  All staging is global_load_lds_dwordx4
+// (lane-linear LDS image, bank swizzle on the source address), retired by counted vmcnt +
+// raw s_barrier.  Layout of the dynamic LDS (16-byte units):
+//   [NR][BM][8] weight ring | [NPB][PXS + 1][8] patches (row PXS of each = zeros)
+// and the epilogue reuses it to transpose each wave's int32 tile (as the gather engine).
+#include <stdlib.h>
+
+#include "tq_device.h"
+#include "tq_epilogue.h"
+#include "tq_launch.h"
+#include "tq_mfma.h"
+
+#ifndef TQ_ABLATE
+#define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
+#endif
+
+namespace tq {
+
+namespace {
+
+constexpr int kPatchBN = 256;       // output pixels per tile
+constexpr int kPatchThreads = 512;  // 8 waves: 2 along Cout x 4 along pixels
+
+struct PatchRows {
+  int64_t base;  // first flattened input row (img * H + iy) of the patch
+  int rows;
+};
+
+// Input rows needed by the tile of output pixels [n0, n0 + 256): the span from the first
+// tap row of its first output row to the last tap row of its last output row (clipped to
+// the images they belong to; rows of images in between are included whole).
+__host__ __device__ inline PatchRows patch_rows(const ConvArgs& a, int64_t n0) {
+  const int64_t n1 = (n0 + kPatchBN < a.P ? n0 + kPatchBN : a.P) - 1;
+  const int64_t fr0 = n0 / a.Wo, fr1 = n1 / a.Wo;
+  const int64_t img0 = fr0 / a.Ho, img1 = fr1 / a.Ho;
+  const int oy0 = (int)(fr0 - img0 * a.Ho), oy1 = (int)(fr1 - img1 * a.Ho);
+  int r0 = oy0 * a.sh - a.ph;
+  int r1 = oy1 * a.sh - a.ph + (a.KH - 1) * a.dh;
+  r0 = r0 < 0 ? 0 : (r0 > a.H - 1 ? a.H - 1 : r0);
+  r1 = r1 < 0 ? 0 : (r1 > a.H - 1 ? a.H - 1 : r1);
+  PatchRows pr;
+  pr.base = img0 * a.H + r0;
+  pr.rows = (int)(img1 * a.H + r1 - pr.base + 1);
+  return pr;
+}
+
+template <int MB, int NR>
+__global__ __launch_bounds__(kPatchThreads, MB == 1 ? 4 : 2) void conv2d_tp_patch_kernel(
+    ConvArgs a) {
+  constexpr int BM = 64 * MB;                 // 2 waves x 32*MB Cout rows
+  constexpr int AI = MB;                      // weight wave-instructions per wave and step
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  const int PXS = a.patch_px;                 // patch slot pixels (multiple of 64)
+  const int PI = PXS / 64;                    // patch wave-instructions per wave and chunk
+  const int NPB = a.patch_bufs;
+  u32x4* ring = lds;
+  u32x4* patch = lds + NR * BM * 8;
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = (a.Cout + BM - 1) / BM;
+  const int64_t ntn = (a.P + kPatchBN - 1) / kPatchBN;
+  const int m0 = (int)(a.m_slow ? tile / ntn : tile % mt) * BM;
+  const int64_t n0 = (a.m_slow ? tile % ntn : tile / mt) * kPatchBN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = (wave >> 2) * 32 * MB;
+  const int wn = (wave & 3) * 64;
+  const int lrow = lane >> 3;
+  const int r32 = lane & 31;
+  const int hh = lane >> 5;
+  const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
+  const uint16_t* __restrict__ wg = reinterpret_cast<const uint16_t*>(a.w);
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page) + lane * 8;
+
+  const PatchRows pr = patch_rows(a, n0);
+  const int PX = pr.rows * a.W;               // host guarantees PX <= PXS
+  const int nch = a.Cp / kKStep;
+  const int ntap = a.KH * a.KW;
+#if TQ_ABLATE == 6
+  const int nsteps = 0;  // timing only: setup + epilogue
+#else
+  const int nsteps = nch * ntap;
+#endif
+
+  // zero row of every patch buffer
+  if (threadIdx.x < 8 * NPB)
+    patch[(threadIdx.x >> 3) * (PXS + 1) * 8 + PXS * 8 + (threadIdx.x & 7)] = (u32x4)0u;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): visible after the first barrier
+
+  // weight rows: this lane's source chunk (swizzled), advanced per step by t*Cp + 64c
+  const uint16_t* arow[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * 8 + lrow;
+    arow[i] = wg + (int64_t)(m0 + r) * a.Kp + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+  }
+  // B fragment pixels: patch index of tap (0, 0) and the mask of in-bounds taps
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  int pix[2];
+  uint64_t tmask[2];
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int64_t n = n0 + wn + 32 * bn + r32;
+    pix[bn] = 0;
+    tmask[bn] = 0;
+    if (n < a.P) {
+      const int64_t img = n / HoWo;
+      const int64_t rem = n - img * HoWo;
+      const int oy = (int)(rem / a.Wo);
+      const int ox = (int)(rem - (int64_t)oy * a.Wo);
+      const int iy0 = oy * a.sh - a.ph;
+      const int ix0 = ox * a.sw - a.pw;
+      pix[bn] = (int)((img * a.H + iy0 - pr.base) * a.W + ix0);
+      for (int r = 0; r < a.KH; ++r) {
+        const int iy = iy0 + r * a.dh;
+        if (iy < 0 || iy >= a.H) continue;
+        for (int q = 0; q < a.KW; ++q) {
+          const int ix = ix0 + q * a.dw;
+          if (ix >= 0 && ix < a.W) tmask[bn] |= 1ull << (r * a.KW + q);
+        }
+      }
+    }
+  }
+
+  auto issue_patch = [&](int c, int buf) {
+    u32x4* dst = patch + buf * (PXS + 1) * 8;
+    for (int j = 0; j < PI; ++j) {
+      const int pp = (wave * PI + j) * 8 + lrow;
+      const uint16_t* src = zero;
+      if (pp < PX)
+        src = xg + ((pr.base * a.W + pp) * a.Cp + c * kKStep + ((lane & 7) ^ ((pp >> 1) & 7)) * 8);
+#if TQ_ABLATE != 3
+      glds16(src, dst + (wave * PI + j) * 64);
+#endif
+    }
+  };
+  auto issue_w = [&](int st, int slot) {
+    const int c = st / ntap;
+    const int t = st - c * ntap;
+    const int64_t off = (int64_t)t * a.Cp + c * kKStep;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+#if TQ_ABLATE != 3
+      glds16(arow[i] + off, ring + slot * BM * 8 + (wave * AI + i) * 64);
+#endif
+    }
+  };
+
+  MfmaAcc<MB> acc;
+  acc_zero(acc);
+  const int kc_steps = a.kc_steps > 0 ? a.kc_steps : (1 << 30);
+  int since_flush = 0;
+
+  // Counted retirement: `issued` counts this wave's LDS-DMA instructions; mark[j] is its
+  // value right after K-step s+j's weight image was issued, so waiting for vmcnt <=
+  // issued - mark[0] retires step s's image and, issued before it, the patch of its chunk.
+  int issued = 0;
+  int mark[NR - 1];
+  issue_patch(0, 0);
+  issued += PI;
+#pragma unroll
+  for (int j = 0; j < NR - 1; ++j) {
+    if (j < nsteps) {
+      issue_w(j, j);
+      issued += AI;
+    }
+    mark[j] = issued;
+  }
+  int c = 0, t = 0, kr = 0, kq = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    wait_vm_dyn(issued - mark[0]);
+#if TQ_ABLATE != 4
+    __builtin_amdgcn_s_barrier();
+#endif
+    if (t == 0 && c + 1 < nch) {
+      issue_patch(c + 1, (c + 1) % NPB);
+      issued += PI;
+    }
+    if (s + NR - 1 < nsteps) {
+      issue_w(s + NR - 1, (s + NR - 1) % NR);
+      issued += AI;
+    }
+#pragma unroll
+    for (int j = 0; j < NR - 2; ++j) mark[j] = mark[j + 1];
+    mark[NR - 2] = issued;
+
+    const u32x4* aimg = ring + (s % NR) * BM * 8;
+    const u32x4* pimg = patch + (c % NPB) * (PXS + 1) * 8;
+    const int toff = kr * a.dh * a.W + kq * a.dw;
+    int prow[2], psw[2];
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+      const int idx = ((tmask[bn] >> t) & 1ull) ? pix[bn] + toff : PXS;
+      prow[bn] = idx * 8;
+      psw[bn] = (idx >> 1) & 7;
+    }
+    // all fragments of the step first (the reads overlap the previous step's MFMAs)
+    half8 af[4][MB], bf[4][2];
+#if TQ_ABLATE == 1 || TQ_ABLATE == 5  // timing only: no fragment reads
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int b = 0; b < MB; ++b) af[k][b] = (half8)(_Float16)(s + k + b);
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn) bf[k][bn] = (half8)(_Float16)(prow[bn] + psw[bn] + k);
+    }
+#else
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int ck = 2 * k + hh;
+#pragma unroll
+      for (int b = 0; b < MB; ++b)
+        af[k][b] = __builtin_bit_cast(half8, aimg[swz(wm + 32 * b + r32, ck)]);
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+        bf[k][bn] = __builtin_bit_cast(half8, pimg[prow[bn] + (ck ^ psw[bn])]);
+    }
+#endif
+#if TQ_ABLATE == 2 || TQ_ABLATE == 5  // timing only: no MFMA (fragments kept live)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int bm = 0; bm < MB; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          asm volatile("" ::"v"(af[k][bm]), "v"(bf[k][bn]));
+#else
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int bm = 0; bm < MB; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          acc.f[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[k][bm], bf[k][bn],
+                                                                 acc.f[bm][bn], 0, 0, 0);
+#endif
+    if (++since_flush == kc_steps) {
+      acc_flush(acc);
+      since_flush = 0;
+    }
+    if (++t == ntap) {
+      t = 0;
+      kr = 0;
+      kq = 0;
+      ++c;
+    } else if (++kq == a.KW) {
+      kq = 0;
+      ++kr;
+    }
+  }
+  acc_flush(acc);
+
+  // Epilogue: transpose each wave's (32*MB Cout) x (64 pixel) int32 tile through LDS so that
+  // lanes run along channels: [pixel][8*MB slots of 4 channels], slot swizzled per pixel.
+  __syncthreads();
+  constexpr int SLOTS = 8 * MB;
+  u32x4* tt = lds + wave * 64 * SLOTS;
+  auto phys = [&](int px, int slot) {
+    return px * SLOTS + (slot ^ (MB == 2 ? (px & 15) : ((px >> 1) & 7)));
+  };
+#pragma unroll
+  for (int bm = 0; bm < MB; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u32x4 v;
+        v.x = (uint32_t)acc.i[bm][bn][4 * q];
+        v.y = (uint32_t)acc.i[bm][bn][4 * q + 1];
+        v.z = (uint32_t)acc.i[bm][bn][4 * q + 2];
+        v.w = (uint32_t)acc.i[bm][bn][4 * q + 3];
+        tt[phys(32 * bn + r32, 8 * bm + 2 * q + hh)] = v;
+      }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  const bool vec = (a.Cout & 3) == 0;
+  const int slot = lane % SLOTS;
+  const int co = m0 + wm + 4 * slot;
+  if (co < a.Cout) {
+    double sc[4], sh[4];
+    load_coef(a, co, sc, sh);
+    constexpr int PXI = 64 / SLOTS;  // pixels per wave-instruction
+#pragma unroll 4
+    for (int it = 0; it < SLOTS; ++it) {
+      const int px = it * PXI + lane / SLOTS;
+      const int64_t p = n0 + wn + px;
+      if (p >= a.P) continue;
+      const u32x4 v = tt[phys(px, slot)];
+      const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      emit4_nhwc(a, p, co, acc4, sc, sh, vec);
+    }
+  }
+}
+
+// Largest patch (pixels) over all tiles: the tile pattern repeats every
+// HoWo / gcd(256, HoWo) tiles, so one period (<= HoWo tiles) is enough.
+int64_t max_patch_px(const ConvArgs& a) {
+  const int64_t howo = (int64_t)a.Ho * a.Wo;
+  int64_t g = kPatchBN, r = howo;
+  while (r) {
+    const int64_t t = g % r;
+    g = r;
+    r = t;
+  }
+  const int64_t tiles = (a.P + kPatchBN - 1) / kPatchBN;
+  int64_t period = howo / g;
+  if (period > tiles) period = tiles;
+  if (period > 4096) return -1;
+  int64_t best = 0;
+  for (int64_t j = 0; j < period; ++j) {
+    const PatchRows pr = patch_rows(a, j * kPatchBN);
+    if (pr.rows > best) best = pr.rows;
+  }
+  // the last (partial) tile is a prefix of a full one: never larger
+  return best * a.W;
+}
+
+constexpr int kLdsBytes = 160 * 1024;
+
+// Dynamic LDS of a (MB, NR) launch, or -1 if it does not fit.
+int64_t patch_lds_bytes(int mb, int nr, int64_t px_slot, int bufs) {
+  int64_t bytes = ((int64_t)nr * 64 * mb * 8 + (int64_t)bufs * (px_slot + 1) * 8) * 16;
+  const int64_t epi = (int64_t)8 * 64 * 8 * mb * 16;  // epilogue transpose
+  if (bytes < epi) bytes = epi;
+  return bytes <= kLdsBytes ? bytes : -1;
+}
+
+template <int MB, int NR>
+hipError_t launch_patch_nr(const ConvArgs& a, int64_t bytes, hipStream_t stream) {
+  constexpr int BM = 64 * MB;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv2d_tp_patch_kernel<MB, NR>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t tiles = ((a.P + kPatchBN - 1) / kPatchBN) * ((a.Cout + BM - 1) / BM);
+  conv2d_tp_patch_kernel<MB, NR>
+      <<<dim3((unsigned)tiles), kPatchThreads, (size_t)bytes, stream>>>(a);
+  return hipGetLastError();
+}
+
+// Deepest weight ring (5, 4 or 3 K-step images) that fits beside the patch buffers and that
+// the chunk's taps cover (the patch of chunk c+1 must be issued before the weight image of
+// its first step: ntap >= NR - 1).
+template <int MB>
+hipError_t launch_patch_mb(ConvArgs a, int64_t px, hipStream_t stream) {
+  const int nch = a.Cp / kKStep;
+  const int ntap = a.KH * a.KW;
+  a.patch_px = (int)((px + 63) / 64 * 64);
+  a.patch_bufs = nch > 1 ? 2 : 1;
+  static const char* env = getenv("TQ_PATCH_RING");  // A/B override (tools only)
+  const int want = env ? atoi(env) : 5;
+  for (int nr = want < 5 ? want : 5; nr >= 3; --nr) {
+    const int64_t bytes = patch_lds_bytes(MB, nr, a.patch_px, a.patch_bufs);
+    if (bytes < 0 || ntap < nr - 1) continue;
+    if (nr == 5) return launch_patch_nr<MB, 5>(a, bytes, stream);
+    if (nr == 4) return launch_patch_nr<MB, 4>(a, bytes, stream);
+    return launch_patch_nr<MB, 3>(a, bytes, stream);
+  }
+  return hipErrorInvalidConfiguration;
+}
+
+}  // namespace
+
+bool conv_patch_eligible(const ConvArgs& a, int out_nhwc) {
+  if (!out_nhwc || a.Cp % kKStep != 0 || a.sh != 1 || a.sw != 1) return false;
+  const int ntap = a.KH * a.KW;
+  if (ntap < 2 || ntap > 64 || a.Kp != ntap * a.Cp) return false;
+  const int64_t px = max_patch_px(a);
+  if (px < 0) return false;
+  const int64_t slot = (px + 63) / 64 * 64;
+  return ntap >= 2 && patch_lds_bytes(2, 3, slot, a.Cp > kKStep ? 2 : 1) > 0;
+}
+
+// mb: 1 = 64-row Cout tiles, 2 = 128-row Cout tiles.
+hipError_t launch_conv2d_patch(const ConvArgs& a, int mb, hipStream_t stream) {
+  const int64_t px = max_patch_px(a);
+  if (px < 0) return hipErrorInvalidConfiguration;
+  return mb == 1 ? launch_patch_mb<1>(a, px, stream) : launch_patch_mb<2>(a, px, stream);
+}
+
+}  // namespace tq

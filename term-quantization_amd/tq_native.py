@@ -15,7 +15,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtq_hip.so")
+# TQ_LIB_PATH: an alternative in-tree build of the same library (tools: ablation builds)
+LIB_PATH = os.environ.get("TQ_LIB_PATH") or os.path.join(_HERE, "lib", "libtq_hip.so")
 
 _lib = None
 _lock = threading.Lock()
@@ -225,6 +226,8 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
         epi.codes_b, epi.cp_b = _ptr(codes_b), codes_b.shape[-1]
         epi.sf_b, epi.bits_b, epi.terms_b = float(quant_b[0]), int(quant_b[1]), int(quant_b[2])
         epi.fmt_b = code_format(codes_b)
+    if not config and fmt == CODES_F16 and os.environ.get("TQ_MFMA_CONFIG"):
+        config = int(os.environ["TQ_MFMA_CONFIG"])  # A/B of MFMA tile configs (tools only)
     epi.workspace, epi.split_k, epi.config = _ptr(workspace), int(split_k), int(config)
     epi.workspace_bytes = workspace.numel() * workspace.element_size() if workspace is not None \
         else 0

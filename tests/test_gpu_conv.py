@@ -112,11 +112,12 @@ def test_act_codes_bit_exact(dtype):
         assert torch.equal(got.long().permute(0, 3, 1, 2), torch.from_numpy(exp_codes))
 
 
-def _engines_pair(cin, cout, ksz, stride, pad, x, db, dt, wb, g, k, sf_x, w=None, seed=0):
+def _engines_pair(cin, cout, ksz, stride, pad, x, db, dt, wb, g, k, sf_x, w=None, seed=0,
+                  dil=1):
     """The same layer built on both engines, run on x; returns (mfma layer, y_mfma, y_valu)."""
     import os
     torch.manual_seed(seed)
-    conv = torch.nn.Conv2d(cin, cout, ksz, stride, pad, bias=True)
+    conv = torch.nn.Conv2d(cin, cout, ksz, stride, pad, dil, bias=True)
     if w is not None:
         with torch.no_grad():
             conv.weight.copy_(w)
@@ -157,6 +158,24 @@ def test_mfma_engine_bit_identical_to_valu(layer):
     lay, ym, yv = _engines_pair(cin, cout, ksz, s, ksz // 2, x, 9, 3, 9, 8, 12, 0.02,
                                 seed=layer)
     assert lay.kc_steps >= 0
+    assert torch.equal(ym, yv)
+
+
+@pytest.mark.parametrize("shape", [
+    # n, cin, h, w, cout, k, pad, dil -- stride 1: the MFMA input-patch engine
+    (37, 128, 5, 5, 96, 3, 1, 1),    # tiles span many images, 2 channel chunks, Cout % 128
+    (3, 64, 9, 11, 64, 5, 2, 1),     # 5x5 taps, one chunk (single patch buffer)
+    (2, 192, 13, 7, 128, 3, 2, 2),   # dilation 2, 3 chunks, non-square
+    (4, 64, 6, 6, 32, 3, 0, 1),      # no padding, Cout < 64
+    (5, 256, 14, 14, 256, 3, 1, 1),  # ResNet layer3 shape
+    (9, 512, 7, 7, 512, 3, 1, 1),    # ResNet layer4 shape
+])
+def test_mfma_patch_engine_bit_identical_to_valu(shape):
+    n, cin, h, w_, cout, ksz, pad, dil = shape
+    torch.manual_seed(sum(shape))
+    x = torch.relu(torch.randn(n, cin, h, w_, device=DEV)).to(memory_format=torch.channels_last)
+    lay, ym, yv = _engines_pair(cin, cout, ksz, 1, pad, x, 9, 3, 9, 8, 12, 0.02,
+                                seed=sum(shape), dil=dil)
     assert torch.equal(ym, yv)
 
 

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import tq_native  # noqa: E402
 import tq_ops  # noqa: E402
 import tr_layer  # noqa: E402
-from microbench import RESNET18_TR, time_fn  # noqa: E402
+from microbench import RESNET18_TR, make_layer, time_fn  # noqa: E402
 
 
 def main():
@@ -29,8 +29,8 @@ def main():
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     cin, cout, k, s, hin = RESNET18_TR[args.layer - 1]
-    conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(dev)
-    layer = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    args.kc = None
+    layer = make_layer(cin, cout, k, s, dev, args)
     cp = tq_ops.act_channels(cin)
     xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
         memory_format=torch.channels_last)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# SQ / GRBM counters for one conv layer config (tools/conv_probe.py), separate passes.
+# SQ / TA / GRBM counters for one conv layer config (tools/conv_probe.py), separate passes.
+# Usage: bash tools/gpu_sq.sh <tag> [conv_probe args...]
 set -u
 TAG=${1:-sq}; shift || true
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -9,11 +10,13 @@ export TMPDIR=/tmp
 cd "$R"
 timeout -k 10 120 python tools/conv_probe.py "$@" > "$O/probe.txt" 2>&1 || { cat "$O/probe.txt"; exit 1; }
 cat "$O/probe.txt"
+timeout -k 10 60 rocprofv3 -L > "$O/counters.txt" 2>&1 || true
 i=0
 for SET in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
-           "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT"; do
+           "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT" \
+           ${EXTRA_SETS:-}; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $SET --output-format csv -d "$O/p$i" -o p -- \
+  timeout -s KILL 120 rocprofv3 --pmc $SET --output-format csv -d "$O/p$i" -o p -- \
       python3 "$R/tools/conv_probe.py" --iters 3 "$@" > "$O/p$i.log" 2>&1 || { tail -5 "$O/p$i.log"; exit 1; }
 done
 echo done

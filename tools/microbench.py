@@ -39,11 +39,23 @@ def time_fn(fn, iters, warmup=3):
     return start.elapsed_time(end) / iters * 1e-3
 
 
+def make_layer(cin, cout, k, s, dev, args):
+    """A ResNet-18 TR conv as the bench builds it (Kaiming-normal fan_out init)."""
+    conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False)
+    torch.nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+    layer = tr_layer.TRConv2dLayer(conv.to(dev), 9, 3, 9, 8, 12)
+    if args.kc is not None and layer.engine == "mfma":
+        layer.kc_steps = args.kc  # timing only: results may be inexact
+    return layer
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--engine", choices=("mfma", "valu"), default="mfma")
+    ap.add_argument("--kc", type=int, default=None,
+                    help="timing only: override the MFMA flush interval (0 = no flush)")
     ap.add_argument("--sweep", action="store_true",
                     help="time every tile config x K-split per layer (fused NHWC entry)")
     args = ap.parse_args()
@@ -70,8 +82,7 @@ def main():
 
     total_mac, total_t = 0, 0.0
     for i, (cin, cout, k, s, hin) in enumerate(RESNET18_TR):
-        conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(dev)
-        layer = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+        layer = make_layer(cin, cout, k, s, dev, args)
         layer.input_quant.tracking = False
         layer.input_quant.sf = 0.02
         xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
@@ -110,8 +121,7 @@ def sweep(args, dev):
             best_total += seen[key][0]
             auto_total += seen[key][1]
             continue
-        conv = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(dev)
-        layer = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+        layer = make_layer(cin, cout, k, s, dev, args)
         cp = tq_ops.act_channels(cin)
         xi = torch.relu(torch.randn(args.batch, cin, hin, hin, device=dev)).to(
             memory_format=torch.channels_last)

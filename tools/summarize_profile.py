@@ -8,8 +8,9 @@ refreshes profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
 
 HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE come from
 separate --pmc passes, both in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
-(16 B/lane) coalesced read, so it is doubled for the TQ kernels (all of whose global loads
-are 16-byte vectors); WRITE_SIZE is exact for 16-byte stores.
+(16 B/lane) coalesced read (global_load and LDS-DMA alike), so it is doubled for the TQ
+kernels (all of whose global loads are 16-byte vectors); WRITE_SIZE is exact for 16-byte
+stores.
 """
 import collections
 import csv
@@ -21,6 +22,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {
     "conv2d_tp": "conv2d_tp_kernel",
+    "conv2d_tp_mfma": "conv2d_tp_mfma",
     "act_encode": "act_encode_kernel",
     "stem_pool_encode": "bn_relu_maxpool_encode_kernel",
     "tr_elem": "tr_elem_kernel",
@@ -67,11 +69,13 @@ def main(tag):
     with open(os.path.join(dst, "%s_summary.json" % tag), "w") as fp:
         json.dump(summary, fp, indent=1)
     conv = summary["kernels"].get("conv2d_tp", {})
+    conv_m = summary["kernels"].get("conv2d_tp_mfma", {})
     enc = summary["kernels"].get("act_encode", {})
     stem = summary["kernels"].get("stem_pool_encode", {})
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as fp:
         json.dump({"source": "profiles/%s_summary.json" % tag,
                    "conv2d_tp_bytes_per_launch": conv.get("hbm_bytes_per_launch"),
+                   "conv2d_tp_mfma_bytes_per_launch": conv_m.get("hbm_bytes_per_launch"),
                    "act_encode_bytes_per_launch": enc.get("hbm_bytes_per_launch"),
                    "stem_pool_encode_bytes_per_launch": stem.get("hbm_bytes_per_launch")}, fp,
                   indent=1)
