@@ -169,6 +169,10 @@ int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int
  * `kc_steps` >= 1 such that for every weight row m and every window of kc_steps K-steps of
  * 64 codes, max|act_code| * sum_{k in window} |w_codes[m][k]| < 2^24 (0 = the whole K
  * range satisfies it), and max_m sum_k |w_codes[m][k]| * max|act_code| < 2^31.
+ * Kernels that walk K chunk-major (the input-patch engine: for each 64-code channel chunk,
+ * all filter taps) use `kc_chunk` instead: the same bound over every window of kc_chunk
+ * consecutive taps of one chunk (0 = never needed; -1 = derive a conservative value from
+ * kc_steps); they also flush at every chunk end.
  *   act_codes  [n][h][w][cp] fp16 codes, 16-byte aligned
  *   w_codes    [cout_pad][kp] fp16 codes, cout_pad a multiple of tq_conv2d_cout_align(),
  *              kp a multiple of 64
@@ -183,8 +187,8 @@ int tq_conv2d_termpair_f16(const uint16_t *act_codes, int64_t n, int64_t h, int6
                            int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
                            int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
                            double scale, const float *bias, float *out, int64_t ho, int64_t wo,
-                           int32_t out_nhwc, int32_t kc_steps, const tq_conv_epilogue *epi,
-                           void *stream);
+                           int32_t out_nhwc, int32_t kc_steps, int32_t kc_chunk,
+                           const tq_conv_epilogue *epi, void *stream);
 
 /*
  * Depthwise term-pair Conv2d (groups == C_in == C_out): per output channel c,

@@ -224,12 +224,14 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->codes_a = epi->codes_a;
   a->cp_a = (int)epi->cp_a;
   a->sf_a = epi->sf_a;
+  a->inv_a = 1.0 / (double)epi->sf_a;
   a->maxv_a = (float)((1u << (epi->codes_a ? epi->bits_a : 0)) - 1u);
   a->k_a = epi->terms_a < 0 ? 0 : epi->terms_a;
   a->fmt_a = epi->fmt_a;
   a->codes_b = epi->codes_b;
   a->cp_b = (int)epi->cp_b;
   a->sf_b = epi->sf_b;
+  a->inv_b = 1.0 / (double)epi->sf_b;
   a->maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
   a->k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
   a->fmt_b = epi->fmt_b;
@@ -282,8 +284,8 @@ int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int6
                            int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
                            int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
                            double scale, const float* bias, float* out, int64_t ho, int64_t wo,
-                           int32_t out_nhwc, int32_t kc_steps, const tq_conv_epilogue* epi,
-                           void* stream) {
+                           int32_t out_nhwc, int32_t kc_steps, int32_t kc_chunk,
+                           const tq_conv_epilogue* epi, void* stream) {
   tq::ConvArgs a;
   int rc = conv_common(reinterpret_cast<const int16_t*>(act_codes), n, h, w, cp,
                        reinterpret_cast<const int16_t*>(w_codes), cout, kh, kw, kp, stride_h,
@@ -293,6 +295,10 @@ int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int6
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_f16: kp must be a multiple of 64");
   if (kc_steps < 0) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_f16: kc_steps must be >= 0");
   a.kc_steps = kc_steps;
+  // chunk-major window: n consecutive taps of one chunk span (n - 1) * (cp / 64) + 1 packed
+  // K-steps, so the conservative derivation keeps them inside one kc_steps window
+  const int64_t nch = cp / 64 > 0 ? cp / 64 : 1;
+  a.kc_chunk = kc_chunk >= 0 ? kc_chunk : (kc_steps > 0 ? (int)((kc_steps - 1) / nch + 1) : 0);
   if (epi == nullptr) {
     if (out == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: out is null");
   } else {
@@ -388,12 +394,14 @@ int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, i
   a.fmt_a = fmt_a;
   a.cp_a = (int)cp_a;
   a.sf_a = sf_a;
+  a.inv_a = 1.0 / (double)sf_a;
   a.maxv_a = (float)((1u << (codes_a ? bits_a : 0)) - 1u);
   a.k_a = terms_a < 0 ? 0 : terms_a;
   a.codes_b = static_cast<int16_t*>(codes_b);
   a.fmt_b = fmt_b;
   a.cp_b = (int)cp_b;
   a.sf_b = sf_b;
+  a.inv_b = 1.0 / (double)sf_b;
   a.maxv_b = (float)((1u << (codes_b ? bits_b : 0)) - 1u);
   a.k_b = terms_b < 0 ? 0 : terms_b;
   return hip_status(tq::launch_bn_relu_maxpool_encode(a, (hipStream_t)stream),

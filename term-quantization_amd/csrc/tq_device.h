@@ -18,11 +18,34 @@ constexpr int kMaxBitwidth = 24;   // keeps every partial sum exact in fp32 (DES
 //   q = min(sat_int32(double(fp32(|x| / sf)) + 0.5), 2^bw - 1), NaN -> 0.
 // The +0.5 is a double add in the reference (the literal 0.5 promotes); doing it in fp32
 // rounds |x|/sf = 0.49999997f up to 1.  With maxv <= 2^24 - 1 (exact in fp32) the
-// reference's fminf(float(int), maxv) round trip equals an integer min, so clamping the
-// double before the conversion gives the same q for every input, +-inf and NaN included.
+// reference's fminf(float(int), maxv) round trip equals an integer min.
+//
+// Both steps are computed without the IEEE fp32 division sequence and without fp64 adds:
+//  * fp32(|x| / sf) == fp32(double(|x|) * RN64(1/sf)).  The double product is within
+//    2^-52 (relative) of the exact quotient, while an exact quotient of two fp32 numbers
+//    that is not itself a rounding midpoint lies at least ~2^-49 (relative) away from every
+//    fp32 midpoint (its distance is (a - m*b)/b, a nonzero multiple of the 49-bit grid of
+//    m*b), and it is never a midpoint in the normal range (odd part of m*b >= 2^24 + 1 >
+//    odd part of a).  So both round to the same fp32 value; the only exceptions are
+//    quotients below 2^-126, which quantize to 0 either way.  
+//  * floor(double(r) + 0.5) == floor(r) + (r - floor(r) >= 0.5) exactly in fp32 (r - floor(r)
+//    is exact; for r >= 2^23 r is an integer and the fraction is 0).
+__device__ __forceinline__ float quotient_f32(float ax, double inv_sf) {
+  return (float)((double)ax * inv_sf);
+}
+
+__device__ __forceinline__ uint32_t round_half_up_clamp(float r, float maxv) {
+  const float fl = floorf(r);
+  const float q0 = fl + ((r - fl) >= 0.5f ? 1.0f : 0.0f);  // +inf stays +inf (NaN compare)
+  return (r == r) ? (uint32_t)fminf(q0, maxv) : 0u;
+}
+
+__device__ __forceinline__ uint32_t quantize_mag_inv(float x, double inv_sf, float maxv) {
+  return round_half_up_clamp(quotient_f32(fabsf(x), inv_sf), maxv);
+}
+
 __device__ __forceinline__ uint32_t quantize_mag(float x, float sf, float maxv) {
-  const double t = (double)(fabsf(x) / sf) + 0.5;
-  return (t == t) ? (uint32_t)fmin(t, (double)maxv) : 0u;
+  return quantize_mag_inv(x, 1.0 / (double)sf, maxv);
 }
 
 // The float64 instantiation of the reference kernel divides in double.
@@ -65,14 +88,22 @@ __device__ __forceinline__ int32_t kept_value(uint32_t pos, uint32_t neg, uint32
   return negative ? -v : v;
 }
 
-// One element through quantize -> encode -> keep top k -> signed integer value.
-template <typename T>
-__device__ __forceinline__ int32_t tr_value_g1(T x, float sf, float maxv, int k) {
-  const uint32_t q = quantize_mag(x, sf, maxv);
+__device__ __forceinline__ int32_t tr_value_of_q(uint32_t q, int k, bool negative) {
   uint32_t pos, neg;
   hese_masks(q, pos, neg);
   const uint32_t keep = keep_top_terms(pos | neg, k);
-  return kept_value(pos, neg, keep, x < (T)0);
+  return kept_value(pos, neg, keep, negative);
+}
+
+// One element through quantize -> encode -> keep top k -> signed integer value.
+template <typename T>
+__device__ __forceinline__ int32_t tr_value_g1(T x, float sf, float maxv, int k) {
+  return tr_value_of_q(quantize_mag(x, sf, maxv), k, x < (T)0);
+}
+
+// fp32 element with a precomputed inv_sf = RN64(1 / sf) (hoisted out of per-element loops).
+__device__ __forceinline__ int32_t tr_value_g1_inv(float x, double inv_sf, float maxv, int k) {
+  return tr_value_of_q(quantize_mag_inv(x, inv_sf, maxv), k, x < 0.0f);
 }
 
 // Activation / weight code formats of the term-pair kernels (include/tq.h TQ_CODES_*):

@@ -31,13 +31,38 @@ __device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4
 }
 
 __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, int co,
-                                             const float y[4], float sf, float maxv, int k,
-                                             int fmt) {
+                                             const float y[4], double inv_sf, float maxv,
+                                             int k, int fmt) {
   uint32_t v[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = code_bits(tr_value_g1(y[i], sf, maxv, k), fmt);
+  for (int i = 0; i < 4; ++i) v[i] = code_bits(tr_value_g1_inv(y[i], inv_sf, maxv, k), fmt);
   *reinterpret_cast<int2*>(codes + p * cp + co) =
       make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+}
+
+// emit4_nhwc with the residual already loaded (rv = residual[p][co..co+3], or zeros when
+// there is none): the epilogue issues every residual load of a tile before its first store,
+// so the loads' latency is paid once, not once per output quad.  Cout % 4 == 0.
+__device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int co,
+                                               const int acc[4], const double sc[4],
+                                               const double sh[4], const float4 rv) {
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
+  if (a.residual) {
+    y[0] += rv.x;
+    y[1] += rv.y;
+    y[2] += rv.z;
+    y[3] += rv.w;
+  }
+  if (a.relu) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+  }
+  if (a.out)
+    *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(y[0], y[1], y[2], y[3]);
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a);
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b);
 }
 
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
@@ -77,8 +102,8 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
         if (co + i < a.Cout) dst[i] = y[i];
     }
   }
-  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.sf_a, a.maxv_a, a.k_a, a.fmt_a);
-  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.sf_b, a.maxv_b, a.k_b, a.fmt_b);
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a);
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b);
 }
 
 // Bijective XCD-aware remap of the block index: blocks are dealt round-robin to the 8 XCDs

@@ -36,16 +36,21 @@ struct ConvArgs {
   int cp_b, k_b;
   float sf_b, maxv_b;
   int fmt_a, fmt_b;     // code formats of codes_a / codes_b (kCodesI16 / kCodesF16)
+  double inv_a, inv_b;  // RN64(1 / sf_a), RN64(1 / sf_b) (set by the C-ABI layer)
   // MFMA engine only: fp32 accumulators are moved into the int32 sums every kc_steps
   // K-steps of 64 codes, a window whose |partial sums| the host has bounded by 2^24 (so
   // every fp32 partial sum is an exact integer); 0 = never needed.
   int kc_steps;
+  // chunk-major engines (patch): the same bound over windows of kc_chunk consecutive taps of
+  // one 64-code channel chunk (fp32 sums also flushed at every chunk end); 0 = never needed
+  int kc_chunk;
   // MFMA patch engine (set by its launcher): patch slot pixels and number of patch buffers
   int patch_px, patch_bufs;
   int m_slow;  // MFMA engines: 1 = Cout tile is the slow index of the tile order
   // Execution choices: config 0 = heuristic, 1..conv_num_configs() = a fixed tile config;
   // splits: 1 data-parallel, > 1 K-split with int32 atomics into ws ([P][Cout]), -1
   // stream-K (ws holds two BM x BN int32 slabs per resident block); NHWC output only.
+  int ab;  // timing-only A/B switches (TQ_AB, tools only; 0 in the product)
   int config, splits;
   int* ws;
   int64_t ws_bytes;
@@ -75,6 +80,7 @@ struct PoolArgs {
   int cp_b, k_b;
   float sf_b, maxv_b;
   int fmt_a, fmt_b;
+  double inv_a, inv_b;   // RN64(1 / sf_a), RN64(1 / sf_b)
 };
 
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
@@ -97,5 +103,8 @@ int conv_mfma_num_configs();
 // MFMA input-patch engine (tr_conv_patch.hip): stride-1 convs with Cp % 64 == 0, NHWC out.
 bool conv_patch_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_patch(const ConvArgs& a, int mb, hipStream_t stream);
+// MFMA direct engine (tr_conv_direct.hip): Cp % 64 == 0, NHWC out; wn = 1 or 2.
+bool conv_direct_eligible(const ConvArgs& a, int out_nhwc);
+hipError_t launch_conv2d_direct(const ConvArgs& a, int wn, hipStream_t stream);
 
 }  // namespace tq

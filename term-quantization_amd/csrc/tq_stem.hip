@@ -57,14 +57,14 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_encode_kernel(PoolArgs a)
   for (int side = 0; side < 2; ++side) {
     int16_t* codes = side ? a.codes_b : a.codes_a;
     if (!codes) continue;
-    const float sf = side ? a.sf_b : a.sf_a;
+    const double inv = side ? a.inv_b : a.inv_a;
     const float maxv = side ? a.maxv_b : a.maxv_a;
     const int k = side ? a.k_b : a.k_a;
     const int cp = side ? a.cp_b : a.cp_a;
     const int fmt = side ? a.fmt_b : a.fmt_a;
     uint32_t b[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = code_bits(tr_value_g1(y[i], sf, maxv, k), fmt);
+    for (int i = 0; i < 8; ++i) b[i] = code_bits(tr_value_g1_inv(y[i], inv, maxv, k), fmt);
     *reinterpret_cast<uint4*>(codes + p * cp + c0) = make_uint4(
         b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
   }

@@ -462,7 +462,8 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // Configs (1-based through ConvArgs.config): 1-2 register-staged (any Cp), 3-6 pipelined
 // gather (Cp % 64 == 0 and KH*KW <= 64; else 1/2), 7-8 input patch (tr_conv_patch.hip:
 // stride 1, KH*KW >= 2, NHWC out; else the gather default).
-int conv_mfma_num_configs() { return 8; }
+// 9-10 direct (tr_conv_direct.hip: Cp % 64 == 0, NHWC out; 256- / 128-pixel tiles).
+int conv_mfma_num_configs() { return 10; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
@@ -473,6 +474,20 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   a.m_slow = ms ? atoi(ms) : 0;
   const bool pipe_ok = a.Cp % kKStep == 0 && a.KH * a.KW <= 64;
   int cfg = a.config > 0 ? a.config - 1 : -1;
+  static const char* ab = getenv("TQ_AB");
+  a.ab = ab ? atoi(ab) : 0;
+  static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 WN
+  if (cfg < 0 && dir && atoi(dir) > 0) cfg = atoi(dir) == 1 ? 9 : 8;
+  // measured (tools/layer_times.py, ResNet-18 batch 256): the direct engine wins where the
+  // fused epilogue dominates -- Cout <= 128 (layer1/2) and 1x1 convs
+  if (cfg < 0 && !(dir && atoi(dir) == 0) && conv_direct_eligible(a, out_nhwc) &&
+      (a.Cout <= 128 || a.KH * a.KW == 1))
+    cfg = 9;
+  if (cfg >= 8) {
+    if (conv_direct_eligible(a, out_nhwc))
+      return launch_conv2d_direct(a, cfg == 8 ? 2 : 1, stream);
+    cfg = -1;
+  }
   if (cfg >= 6 || cfg < 0) {
     if (conv_patch_eligible(a, out_nhwc)) {
       const int mb = cfg == 6 ? 2 : cfg == 7 ? 1 : (a.Cout <= 64 ? 1 : 2);

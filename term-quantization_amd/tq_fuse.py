@@ -57,6 +57,7 @@ class _Conv(object):
         self.scale, self.shift = _fold_bn(layer, bn)
         self.code_dtype = layer.w_codes.dtype   # int16 (VALU engine) / float16 (MFMA engine)
         self.kc_steps = layer.kc_steps
+        self.kc_chunk = layer.kc_chunk
         if self.cout % 4:
             raise ValueError("fused epilogue needs Cout % 4 == 0")
 
@@ -92,7 +93,7 @@ class _Conv(object):
                 ch_shift=self.shift, residual=res, relu=relu, codes_a=ca,
                 quant_a=next_a.quant if next_a else None, codes_b=cb,
                 quant_b=next_b.quant if next_b else None, workspace=ws,
-                kc_steps=self.kc_steps))
+                kc_steps=self.kc_steps, kc_chunk=self.kc_chunk))
         return out, ca, cb
 
 

@@ -69,7 +69,7 @@ _SIGNATURES["tq_conv2d_termpair_fused"] = [
 
 _SIGNATURES["tq_conv2d_termpair_f16"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
-    _i64, _f64, _vp, _vp, _i64, _i64, _i32, _i32, ctypes.POINTER(ConvEpilogue), _vp]
+    _i64, _f64, _vp, _vp, _i64, _i64, _i32, _i32, _i32, ctypes.POINTER(ConvEpilogue), _vp]
 
 # include/tq.h TQ_CODES_*: the code format follows the code tensor's dtype
 CODES_I16 = 0
@@ -167,9 +167,10 @@ def conv2d_cout_align():
 
 
 def conv2d_termpair(codes, w_codes, cout, kh, kw, stride, padding, dilation, scale, bias, out,
-                    out_nhwc, kc_steps=0):
+                    out_nhwc, kc_steps=0, kc_chunk=-1):
     """Plain term-pair conv.  int16 codes run the VALU engine (tq_conv2d_termpair), float16
-    codes the MFMA engine (tq_conv2d_termpair_f16, flush interval ``kc_steps``)."""
+    codes the MFMA engine (tq_conv2d_termpair_f16, flush intervals ``kc_steps`` /
+    ``kc_chunk``)."""
     n, h, w, cp = codes.shape
     ho, wo = out.shape[2], out.shape[3]
     fmt = code_format(codes)
@@ -180,8 +181,8 @@ def conv2d_termpair(codes, w_codes, cout, kh, kw, stride, padding, dilation, sca
             rc = lib().tq_conv2d_termpair_f16(
                 _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],
                 stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1],
-                float(scale), _ptr(bias), _ptr(out), ho, wo, int(out_nhwc), int(kc_steps), None,
-                _stream(codes))
+                float(scale), _ptr(bias), _ptr(out), ho, wo, int(out_nhwc), int(kc_steps),
+                int(kc_chunk), None, _stream(codes))
         else:
             rc = lib().tq_conv2d_termpair(_ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh,
                                           kw, w_codes.shape[1], stride[0], stride[1],
@@ -205,7 +206,7 @@ def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
 def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilation, ho, wo,
                           out=None, ch_scale=None, ch_shift=None, residual=None, relu=False,
                           codes_a=None, quant_a=None, codes_b=None, quant_b=None,
-                          workspace=None, split_k=0, config=0, kc_steps=0):
+                          workspace=None, split_k=0, config=0, kc_steps=0, kc_chunk=-1):
     """Term-pair conv with the fused epilogue of tq_conv2d_termpair_fused (channels_last).
     quant_a/_b = (sf, bits, terms) of the layer consuming codes_a/_b, whose dtype (int16 /
     float16) is that layer's code format.  ``workspace`` (int32, >= n*ho*wo*cout elements)
@@ -236,7 +237,8 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
             rc = lib().tq_conv2d_termpair_f16(
                 _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],
                 stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1], 0.0,
-                None, _ptr(out), ho, wo, 1, int(kc_steps), ctypes.byref(epi), _stream(codes))
+                None, _ptr(out), ho, wo, 1, int(kc_steps), int(kc_chunk), ctypes.byref(epi),
+                _stream(codes))
         else:
             rc = lib().tq_conv2d_termpair_fused(
                 _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],

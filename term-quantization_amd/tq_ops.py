@@ -179,12 +179,37 @@ def mfma_flush_steps(packed, data_bits):
     return 0 if best == s else best
 
 
+def mfma_flush_chunk(packed, data_bits, cp, ntaps):
+    """mfma_flush_steps for kernels that walk K chunk-major (tq.h ``kc_chunk``): the largest
+    n such that every window of n consecutive filter taps of one 64-code channel chunk
+    satisfies 2^data_bits * sum|v_w| <= 2^24 in every row; 0 if a whole chunk qualifies
+    (the kernel also flushes at every chunk end), -1 if not even one step does or if Cp is
+    not a multiple of 64 (no chunk-major kernel runs then; -1 lets the library derive a
+    conservative value from kc_steps)."""
+    if cp % K_ALIGN_MFMA:
+        return -1
+    o_pad, kp = packed.shape
+    nch = cp // K_ALIGN_MFMA
+    steps = packed.double().abs().view(o_pad, kp // K_ALIGN_MFMA, K_ALIGN_MFMA).sum(-1)
+    steps = steps[:, :ntaps * nch].reshape(o_pad, ntaps, nch).permute(0, 2, 1)  # [O, c, tap]
+    lim = float(FP32_EXACT) / float(2**int(data_bits))
+    c = torch.nn.functional.pad(steps.cumsum(2), (1, 0))  # [O, nch, ntaps + 1]
+    best = 0
+    for n in range(1, ntaps + 1):
+        if (c[:, :, n:] - c[:, :, :ntaps + 1 - n]).max().item() > lim:
+            break
+        best = n
+    if best == 0:
+        return -1
+    return 0 if best == ntaps else best
+
+
 def conv_out_size(h, k, s, p, d):
     return (h + 2 * p - d * (k - 1) - 1) // s + 1
 
 
 def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_channels,
-              kernel_size, stride, padding, dilation, kc_steps=0):
+              kernel_size, stride, padding, dilation, kc_steps=0, kc_chunk=-1):
     """conv2d(TR(x), TR(w)) + bias by exact term-pair accumulation (groups = 1).
 
     x: fp32 [N, C, H, W] CUDA tensor, NCHW-contiguous or channels_last.  The output has the
@@ -218,7 +243,7 @@ def tr_conv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_chan
     _launch("conv2d_termpair", n * ho * wo * out_channels * c * kh * kw,
             lambda: tq_native.conv2d_termpair(codes, w_packed, out_channels, kh, kw, stride,
                                               padding, dilation, scale, bias, out, nhwc,
-                                              kc_steps))
+                                              kc_steps, kc_chunk))
     return out
 
 
@@ -276,7 +301,7 @@ def tr_dwconv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, channe
 
 
 def tr_linear(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features,
-              kc_steps=0):
+              kc_steps=0, kc_chunk=-1):
     """linear(TR(x), TR(w)) + bias by exact term-pair accumulation: the rows of x are the
     pixels of a 1x1 term-pair conv (channels_last [M, C, 1, 1] is x's own memory)."""
     shape = x.shape
@@ -284,5 +309,5 @@ def tr_linear(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_feat
     m = x2.shape[0]
     xc = x2.view(m, 1, 1, shape[-1]).permute(0, 3, 1, 2)  # channels_last view, no copy
     y = tr_conv2d(xc, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_features,
-                  (1, 1), (1, 1), (0, 0), (1, 1), kc_steps)
+                  (1, 1), (1, 1), (0, 0), (1, 1), kc_steps, kc_chunk)
     return y.permute(0, 2, 3, 1).reshape(*shape[:-1], out_features)

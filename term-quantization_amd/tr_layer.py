@@ -142,6 +142,13 @@ class LinearQuantize(nn.Module):
         self.tracking = False
 
 
+def _kc_chunk(packed, engine, data_bits, cp, ntaps):
+    """Exactness window for the chunk-major MFMA engine (tq_ops.mfma_flush_chunk)."""
+    if engine != "mfma":
+        return 0
+    return tq_ops.mfma_flush_chunk(packed, data_bits, cp, ntaps)
+
+
 def _pack_termpair(codes, data_bits, weight_bits):
     """Pack int32 weight term sums [O, I, KH, KW] for the layer's term-pair engine:
     (packed, Cp, engine, kc_steps).  MFMA when the codes are exact fp16 values and one K-step
@@ -212,6 +219,8 @@ class TRConv2dLayer(nn.Module):
             elif mode == "termpair":
                 packed, cp, self.engine, self.kc_steps = _pack_termpair(codes, data_bits,
                                                                         weight_bits)
+                self.kc_chunk = _kc_chunk(packed, self.engine, data_bits, cp,
+                                          codes.shape[2] * codes.shape[3])
             else:
                 packed, cp = tq_ops.pack_dw_weight(codes)
         else:
@@ -219,7 +228,7 @@ class TRConv2dLayer(nn.Module):
         self.mode = mode
         self.termpair = mode == "termpair"
         if not self.termpair:
-            self.engine, self.kc_steps = None, 0
+            self.engine, self.kc_steps, self.kc_chunk = None, 0, 0
         self.register_buffer('w_codes', packed)
         if packed is not None:
             self.act_channels = cp
@@ -243,7 +252,7 @@ class TRConv2dLayer(nn.Module):
         return tq_ops.tr_conv2d(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, c.bias,
                                 c.out_channels, c.kernel_size, c.stride, c.padding, c.dilation,
-                                self.kc_steps)
+                                self.kc_steps, self.kc_chunk)
 
     def tracking(self, tracking):
         if not tracking:
@@ -278,7 +287,7 @@ class TRLinearLayer(nn.Module):
         w = linear_layer.weight
         self.w_sf = _w_sf(w, weight_bits)
         self.termpair = False
-        self.engine, self.kc_steps = None, 0
+        self.engine, self.kc_steps, self.kc_chunk = None, 0, 0
         packed = None
         if (quantize_input and weight_bits <= tq_ops.MAX_CODE_BITS
                 and data_bits <= tq_ops.MAX_CODE_BITS and w.dtype == torch.float32):
@@ -288,6 +297,7 @@ class TRLinearLayer(nn.Module):
             if bound < 2**31:
                 packed, self.act_channels, self.engine, self.kc_steps = _pack_termpair(
                     codes[:, :, None, None], data_bits, weight_bits)
+                self.kc_chunk = _kc_chunk(packed, self.engine, data_bits, self.act_channels, 1)
                 self.termpair = True
         else:
             wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
@@ -305,7 +315,7 @@ class TRLinearLayer(nn.Module):
             return self.linear(self.input_quant(x))
         return tq_ops.tr_linear(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, self.linear.bias,
-                                self.linear.out_features, self.kc_steps)
+                                self.linear.out_features, self.kc_steps, self.kc_chunk)
 
     def tracking(self, tracking):
         if not tracking:

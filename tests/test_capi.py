@@ -91,16 +91,16 @@ def test_conv_f16_argument_validation():
     lib = tq_native.lib()
     # kp must be a multiple of 64 for the MFMA engine
     rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 4, 3, 3, 160, 1, 1, 1, 1, 1, 1,
-                                    1.0, None, None, 8, 8, 1, 0, None, None)
+                                    1.0, None, None, 8, 8, 1, 0, -1, None, None)
     assert rc == 1 and b"64" in lib.tq_last_error()
     rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 4, 3, 3, 192, 1, 1, 1, 1, 1, 1,
-                                    1.0, None, None, 8, 8, 1, -1, None, None)
+                                    1.0, None, None, 8, 8, 1, -1, -1, None, None)
     assert rc == 1 and b"kc_steps" in lib.tq_last_error()
     epi = tq_native.ConvEpilogue()
     epi.split_k = 2
     out = ctypes.c_void_p(16)
     rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 4, 3, 3, 192, 1, 1, 1, 1, 1, 1,
-                                    1.0, None, out, 8, 8, 1, 0, ctypes.byref(epi), None)
+                                    1.0, None, out, 8, 8, 1, 0, -1, ctypes.byref(epi), None)
     assert rc == 2 and b"split" in lib.tq_last_error()
     assert lib.tq_conv2d_mfma_num_configs() >= 1
 

@@ -147,3 +147,46 @@ def test_mse_profile_matches_oracle():
 
 def test_library_version():
     assert tq_native.version().startswith("tq-hip")
+
+
+def _near_midpoints(rng, qmax, n_sf=64, per_sf=512):
+    """fp32 inputs whose quotient |x|/sf lies within a few ulps of a rounding midpoint
+    q + 0.5 of the quantizer, for random fp32 scales (normal, tiny and huge) -- the cases
+    where a wrong fp32 quotient would change q."""
+    sfs = np.concatenate([rng.uniform(1e-3, 1.0, n_sf // 2),
+                          10.0 ** rng.uniform(-30, 30, n_sf // 2)]).astype(np.float32)
+    out = []
+    for sf in sfs:
+        q = rng.integers(0, qmax, per_sf).astype(np.float64)
+        mid = ((q + 0.5) * np.float64(sf)).astype(np.float32)
+        steps = rng.integers(-3, 4, per_sf).astype(np.int32)
+        x = mid.view(np.int32) + steps
+        x = x.view(np.float32)
+        x = np.where(rng.random(per_sf) < 0.5, -x, x).astype(np.float32)
+        out.append((float(sf), x))
+    return out
+
+
+@pytest.mark.parametrize("bw", [9, 24])
+def test_tr_quotient_near_midpoints(bw):
+    """The division-free quantizer (fp32(|x| * RN64(1/sf)), tq_device.h) against the
+    oracle's true fp32 division, on quotients a few ulps from every kind of midpoint."""
+    rng = np.random.default_rng(bw)
+    for sf, x in _near_midpoints(rng, 2**bw):
+        x = x.reshape(1, -1, 1, 1)
+        for k in (3, 24):
+            _check(x, sf, bw, 1, k)
+        _check(x.reshape(-1, 8), sf, bw, 8, 12)
+
+
+def test_act_codes_near_midpoints():
+    """Activation codes (tq_act_encode, the epilogue's TR) on the same adversarial inputs."""
+    rng = np.random.default_rng(5)
+    for sf, x in _near_midpoints(rng, 2**14, n_sf=16, per_sf=64 * 16):
+        xt = torch.from_numpy(x.reshape(16, 64, 1, 1)).to(DEV).contiguous(
+            memory_format=torch.channels_last)
+        codes = torch.empty((16, 1, 1, 64), dtype=torch.int16, device=DEV)
+        tq_native.act_encode(xt, True, sf, 14, 3, codes)
+        exp = oracle.tr(x.reshape(1, -1, 1, 1), sf, 14, 1, 3).reshape(16, 64)
+        got = codes.cpu().numpy().reshape(16, 64).astype(np.float32) * np.float32(sf)
+        np.testing.assert_array_equal(got, exp)
