@@ -10,21 +10,21 @@
 // Why this shape.  The ResNet-18 TQ convs are short-K (576-4608) and their fused epilogue
 // (BN fold, residual, ReLU, fp32 output, next layers' TR codes) moves more bytes than the
 // main loop: a kernel that runs one workgroup per CU serialises patch load -> MFMA ->
-// epilogue.  Here a workgroup needs only 16 KB of LDS and <= 256 VGPRs per lane, so two
-// (or more) workgroups share a CU and one's epilogue overlaps the other's main loop.
+// epilogue.  Here a 128-pixel workgroup needs 33 KB of LDS and ~150 VGPRs per lane, so three
+// workgroups share a CU and one's epilogue overlaps the others' main loops.
 //
 //   workgroup = 4 waves, tile 64 (Cout) x 4*32*WN (output pixels)
 //   wave      = 64 x 32*WN: 2 x WN MFMA blocks of 32 x 32, 8*WN MFMAs per K-step
 //   K-step    = 64 codes of one filter tap (Cp % 64 == 0)
-//   A (weights [Cout_pad][Kp] fp16): global_load_lds_dwordx4 into a 2-slot ring, 8 KB/slot,
+//   A (weights [Cout_pad][Kp] fp16): global_load_lds_dwordx4 into a 3-slot ring, 8 KB/slot,
 //             rows swizzled chunk ^= (row >> 1) & 7 on the source side (conflict-free reads)
 //   B (activation codes [N][H][W][Cp] fp16): lane (r32, hh) loads, per block column and
 //             16-code substep s, the 16 bytes [16s + 8hh, +8) of its pixel at the step's tap;
-//             taps in the zero padding read a zero page; next step's loads are in flight
-//             during the current step's MFMAs (register double buffer)
-//   epilogue: straight from the MFMA layout (lane = pixel, 4 consecutive channels per
-//             register quad): every residual load of the wave tile issued first, per-channel
-//             (scale, shift) from LDS, 16-byte fp32 stores, 8-byte code stores.
+//             taps in the zero padding read a zero page; the next two steps' loads are in
+//             flight during the current step's MFMAs (register triple buffer, counted vmcnt)
+//   epilogue: every residual load of the wave tile issued first, then the int32 tile is
+//             transposed through LDS so 16 lanes cover one pixel's 64 channels: each store
+//             instruction writes 4 whole pixel rows (fp32 out: 1 KB, codes: 512 B).
 #include "tq_device.h"
 #include "tq_epilogue.h"
 #include "tq_launch.h"
@@ -36,25 +36,36 @@ namespace {
 
 constexpr int kDirThreads = 256;
 constexpr int kDirBM = 64;
+constexpr int kDirSlots = 3;  // A ring depth = K-steps in flight + 1
+
+template <int WN>
+struct DirCfg {
+  static constexpr int BN = 4 * 32 * WN;
+  static constexpr int SLOT = kDirBM * 8;          // u32x4 per A slot (64 rows x 128 B)
+  static constexpr int TILE = 64 * 32 * WN / 4;    // u32x4 per wave epilogue tile (int32)
+  static constexpr int LDS = kDirSlots * SLOT > 4 * TILE ? kDirSlots * SLOT : 4 * TILE;
+  static constexpr int LPS = 2 + 4 * WN;           // vmem instructions per wave and K-step
+};
 
 template <int WN, bool FLUSH>
-__global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
-  constexpr int BN = 4 * 32 * WN;
-  constexpr int SLOT = kDirBM * 8;  // u32x4 per A slot (64 rows x 128 B)
-  __shared__ __attribute__((aligned(16))) u32x4 ring[2 * SLOT];
+__global__ __launch_bounds__(kDirThreads, WN == 1 ? 2 : 1) void conv2d_tp_direct_kernel(
+    ConvArgs a) {
+  using C = DirCfg<WN>;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
   __shared__ double coef[kDirBM][2];  // epilogue (scale, shift) of the tile's channels
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = (a.Cout + kDirBM - 1) / kDirBM;
   const int m0 = (tile % mt) * kDirBM;
-  const int64_t n0 = (int64_t)(tile / mt) * BN;
+  const int64_t n0 = (int64_t)(tile / mt) * C::BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r32 = lane & 31;
   const int hh = lane >> 5;
+  const int64_t wn0 = n0 + wave * 32 * WN;  // first pixel of this wave
   const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
   const uint16_t* __restrict__ wg = reinterpret_cast<const uint16_t*>(a.w);
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page);
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page) + 8 * hh;
 
   // A staging: wave w moves rows [16w, 16w + 16) of each slot, 2 wave-instructions of 8 rows
   const uint16_t* arow[2];
@@ -71,7 +82,7 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   uint64_t tmask[WN];
 #pragma unroll
   for (int bn = 0; bn < WN; ++bn) {
-    const int64_t p = n0 + wave * 32 * WN + 32 * bn + r32;
+    const int64_t p = wn0 + 32 * bn + r32;
     boff[bn] = 0;
     tmask[bn] = 0;
     if (p < a.P) {
@@ -101,27 +112,39 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
                                       : ((a.bias && ok) ? (double)a.bias[co] : 0.0);
   }
 
-  const int nch = a.Cp / kKStep;
-  const int nsteps = a.Kp / kKStep;  // taps * nch, plus zero K padding steps (tap >= KH*KW)
+  const int nsteps = a.Kp / kKStep;  // = KH * KW * Cp / 64 (Cp % 64 == 0)
+  // position of the next K-step to issue, advanced incrementally (no divisions in the loop)
+  int i_st = 0, i_tap = 0, i_cb = 0, i_ks = 0;
+  int64_t i_toff = 0;  // ((kr * dh) * W + ks * dw) * Cp + cb
+  const int64_t row_step = (int64_t)a.dh * a.W * a.Cp;
+  const int64_t col_step = (int64_t)a.dw * a.Cp;
+  int64_t row_off = 0;
 
-  auto issue_a = [&](int st, int slot) {
+  // Issue K-step i_st: A-DMA into `slot`, B fragments into b (lane: codes [16s + 8hh, +8)).
+  auto issue = [&](int slot, u32x4 (&b)[WN][4]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      glds16(arow[i] + (int64_t)st * kKStep, ring + slot * SLOT + (wave * 2 + i) * 64);
-  };
-  // B fragments of K-step st: b[bn][s] = codes [16s + 8hh, +8) of block column bn's pixel
-  auto load_b = [&](int st, u32x4 (&b)[WN][4]) {
-    const int tap = st / nch;
-    const int cb = (st - tap * nch) * kKStep;
-    const int kr = tap / a.KW;
-    const int ks = tap - kr * a.KW;
-    const int64_t toff = ((int64_t)kr * a.dh * a.W + (int64_t)ks * a.dw) * a.Cp + cb;
+      glds16(arow[i] + (int64_t)i_st * kKStep, lds + slot * C::SLOT + (wave * 2 + i) * 64);
 #pragma unroll
     for (int bn = 0; bn < WN; ++bn) {
-      const bool ok = (tmask[bn] >> tap) & 1ull;  // tap >= KH*KW: bit clear
-      const uint16_t* src = ok ? xg + (boff[bn] + toff) : zero + 8 * hh;
+      const bool ok = (tmask[bn] >> i_tap) & 1ull;
+      const uint16_t* src = ok ? xg + (boff[bn] + i_toff) : zero;
 #pragma unroll
       for (int s = 0; s < 4; ++s) b[bn][s] = *reinterpret_cast<const u32x4*>(src + 16 * s);
+    }
+    ++i_st;
+    i_cb += kKStep;
+    i_toff += kKStep;
+    if (i_cb == a.Cp) {
+      i_cb = 0;
+      ++i_tap;
+      if (++i_ks == a.KW) {
+        i_ks = 0;
+        row_off += row_step;
+        i_toff = row_off;
+      } else {
+        i_toff = row_off + (int64_t)i_ks * col_step;
+      }
     }
   };
 
@@ -130,15 +153,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   const int kc_steps = a.kc_steps;
   int since_flush = 0;
 
-  u32x4 b0[WN][4], b1[WN][4];
-  auto step = [&](int s, u32x4 (&bc)[WN][4], u32x4 (&bnx)[WN][4]) {
-    TQ_WAIT_VM(0);  // this wave's A-DMA and B loads of step s have landed
-    __builtin_amdgcn_s_barrier();  // every wave's A-DMA of step s landed; slot s^1 is free
-    if (s + 1 < nsteps) {
-      issue_a(s + 1, (s + 1) & 1);
-      load_b(s + 1, bnx);
-    }
-    const u32x4* img = ring + (s & 1) * SLOT;
+  auto compute = [&](int slot, const u32x4 (&bc)[WN][4]) {
+    const u32x4* img = lds + slot * C::SLOT;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int c = 2 * k + hh;
@@ -161,82 +177,84 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     }
   };
 
-  issue_a(0, 0);
-  load_b(0, b0);
+  // Two K-steps in flight: step s is retired by vmcnt(LPS) (only step s + 1 younger), a
+  // barrier makes every wave's A-DMA of step s visible and frees slot (s + 2) % 3.
+  u32x4 b0[WN][4], b1[WN][4], b2[WN][4];
+  auto step = [&](int s, int slot, const u32x4 (&bc)[WN][4], u32x4 (&bnext)[WN][4]) {
+    if (s + 1 < nsteps) TQ_WAIT_VM(C::LPS);
+    else TQ_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < nsteps) issue((slot + 2) % kDirSlots, bnext);
+    compute(slot, bc);
+  };
+  issue(0, b0);
+  if (nsteps > 1) issue(1, b1);
   int s = 0;
-  for (; s + 1 < nsteps; s += 2) {
-    step(s, b0, b1);
-    step(s + 1, b1, b0);
+  for (; s + 2 < nsteps; s += 3) {
+    step(s, 0, b0, b2);
+    step(s + 1, 1, b1, b0);
+    step(s + 2, 2, b2, b1);
   }
-  if (s < nsteps) step(s, b0, b1);
+  if (s < nsteps) step(s, 0, b0, b2);
+  if (s + 1 < nsteps) step(s + 1, 1, b1, b0);
   acc_flush(acc);
 
-  // Epilogue: block (bn, bm), register quad q of lane (r32, hh) = pixel 32*bn + r32 of the
-  // wave, channels 32*bm + 8q + 4hh .. +3.  Residual loads for the whole wave tile are issued
-  // first (one latency), per-channel coefficients come from LDS.
-  __syncthreads();  // coef[] is visible (also when the K loop was empty)
+  // Epilogue.  Lane (slot = lane & 15) finishes channels m0 + 4*slot .. +3 of pixels
+  // it*4 + (lane >> 4) of its wave: each store instruction writes 4 whole pixel rows.
   const bool vec = (a.Cout & 3) == 0;
-  if (!vec) {
+  const int slot = lane & 15;
+  const int co = m0 + 4 * slot;
+  float4 res[8 * WN];  // residuals first: their latency overlaps the transpose
+#pragma unroll
+  for (int it = 0; it < 8 * WN; ++it) {
+    const int64_t p = wn0 + it * 4 + (lane >> 4);
+    res[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec && a.residual && co < a.Cout && p < a.P)
+      res[it] = *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co);
+  }
+  __syncthreads();  // every wave is done with the A ring; coef[] is visible
+  u32x4* t = lds + wave * C::TILE;  // [pixel][16 slots of 4 channels], slot ^= pixel & 15
+#pragma unroll
+  for (int bn = 0; bn < WN; ++bn)
 #pragma unroll
     for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int co = m0 + 32 * bm + 8 * q + 4 * hh;
-        if (co >= a.Cout) continue;
-        double sc[4], sh[4];
-        load_coef(a, co, sc, sh);
-#pragma unroll
-        for (int bn = 0; bn < WN; ++bn) {
-          const int64_t p = n0 + wave * 32 * WN + 32 * bn + r32;
-          if (p >= a.P) continue;
-          const int acc4[4] = {acc.i[bn][bm][4 * q], acc.i[bn][bm][4 * q + 1],
-                               acc.i[bn][bm][4 * q + 2], acc.i[bn][bm][4 * q + 3]};
-          emit4_nhwc(a, p, co, acc4, sc, sh, false);
-        }
+        const int px = 32 * bn + r32;
+        const int sl = 8 * bm + 2 * q + hh;  // channels 32bm + 8q + 4hh .. +3
+        u32x4 v;
+        v.x = (uint32_t)acc.i[bn][bm][4 * q];
+        v.y = (uint32_t)acc.i[bn][bm][4 * q + 1];
+        v.z = (uint32_t)acc.i[bn][bm][4 * q + 2];
+        v.w = (uint32_t)acc.i[bn][bm][4 * q + 3];
+        t[px * 16 + (sl ^ (px & 15))] = v;
       }
-    return;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
+  __builtin_amdgcn_wave_barrier();
+  if (co >= a.Cout) return;
+  double sc[4], sh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sc[i] = coef[4 * slot + i][0];
+    sh[i] = coef[4 * slot + i][1];
   }
-  float4 res[2][4][WN];
 #pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int bn = 0; bn < WN; ++bn) {
-        const int co = m0 + 32 * bm + 8 * q + 4 * hh;
-        const int64_t p = n0 + wave * 32 * WN + 32 * bn + r32;
-        res[bm][q][bn] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a.residual && co < a.Cout && p < a.P)
-          res[bm][q][bn] = *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co);
-      }
-#pragma unroll
-  for (int bm = 0; bm < 2; ++bm) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int cl = 32 * bm + 8 * q + 4 * hh;  // channel within the tile
-      const int co = m0 + cl;
-      if (co >= a.Cout) continue;
-      double sc[4], sh[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        sc[i] = coef[cl + i][0];
-        sh[i] = coef[cl + i][1];
-      }
-#pragma unroll
-      for (int bn = 0; bn < WN; ++bn) {
-        const int64_t p = n0 + wave * 32 * WN + 32 * bn + r32;
-        if (p >= a.P) continue;
-        const int acc4[4] = {acc.i[bn][bm][4 * q], acc.i[bn][bm][4 * q + 1],
-                             acc.i[bn][bm][4 * q + 2], acc.i[bn][bm][4 * q + 3]};
-        emit4_nhwc_res(a, p, co, acc4, sc, sh, res[bm][q][bn]);
-      }
-    }
+  for (int it = 0; it < 8 * WN; ++it) {
+    const int px = it * 4 + (lane >> 4);
+    const int64_t p = wn0 + px;
+    if (p >= a.P) continue;
+    const u32x4 v = t[px * 16 + (slot ^ (px & 15))];
+    const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+    if (vec)
+      emit4_nhwc_res(a, p, co, acc4, sc, sh, res[it]);
+    else
+      emit4_nhwc(a, p, co, acc4, sc, sh, false);
   }
 }
 
 template <int WN, bool FLUSH>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
-  constexpr int BN = 4 * 32 * WN;
+  constexpr int BN = DirCfg<WN>::BN;
   const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + kDirBM - 1) / kDirBM);
   conv2d_tp_direct_kernel<WN, FLUSH><<<dim3((unsigned)tiles), kDirThreads, 0, stream>>>(a);
   return hipGetLastError();

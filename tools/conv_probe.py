@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--split", type=int, default=0)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--codes", type=int, default=0, help="next-layer code outputs (0-2)")
+    ap.add_argument("--residual", action="store_true", help="fp32 residual input")
+    ap.add_argument("--no-out", action="store_true", help="no fp32 output (codes only)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -41,10 +44,20 @@ def main():
     ws = tq_native.conv2d_workspace(args.batch * ho * ho, cout, dev)
     sc = torch.full((cout,), 1e-4, dtype=torch.float64, device=dev)
     sh = torch.zeros(cout, dtype=torch.float64, device=dev)
+    res = torch.randn_like(o) if args.residual else None
+    cpo = tq_ops.act_channels(cout)
+    ca = torch.empty((args.batch, ho, ho, cpo), dtype=codes.dtype, device=dev) \
+        if args.codes >= 1 else None
+    cb = torch.empty_like(ca) if args.codes >= 2 else None
+    q = (0.05, 9, 3)
     fn = lambda: tq_native.conv2d_termpair_fused(
-        codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho, out=o,
-        ch_scale=sc, ch_shift=sh, workspace=None if layer.engine == "mfma" else ws,
-        split_k=args.split, config=args.config, kc_steps=layer.kc_steps)
+        codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho,
+        out=None if args.no_out else o, ch_scale=sc, ch_shift=sh, residual=res, relu=True,
+        codes_a=ca, quant_a=q if ca is not None else None, codes_b=cb,
+        quant_b=q if cb is not None else None,
+        workspace=None if layer.engine == "mfma" else ws,
+        split_k=args.split, config=args.config, kc_steps=layer.kc_steps,
+        kc_chunk=getattr(layer, "kc_chunk", -1))
     t = time_fn(fn, args.iters)
     mac = args.batch * cout * ho * ho * cin * k * k
     print("layer %d cfg %d split %d: %.1f us  %.1f TMAC/s" % (args.layer, args.config,
