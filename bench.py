@@ -41,6 +41,7 @@ DOT2_PEAK = 2 * VALU_LANE_OPS / 2   # 78.6e12 term-sum MAC/s
 # v_mfma_f32_32x32x16_f16: dense fp16 MFMA peak (MI355X_MICROARCH.md, matrix cores; the
 # 2:1-sparsity headline is not a dense rate) -- 2 FLOP per term-sum product
 MFMA_F16_PEAK_TFLOPS = 2500.0
+FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 vector / f32-MFMA peak (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -256,7 +257,8 @@ def main():
         conv = kt["conv2d_termpair"]
         # the HBM-bound TR stage of the step: the fused stem tail (BN/ReLU/max-pool + the
         # first TR layer's activation TR) in the fused executor, act_encode otherwise
-        enc_name = "stem_pool_encode" if "stem_pool_encode" in kt else "act_encode"
+        enc_name = next(k for k in ("stem_conv_pool", "stem_pool_encode", "act_encode")
+                        if k in kt)
         enc = kt[enc_name]
         conv_t = conv["seconds"] / conv["launches"]
         conv_work = conv["work"] / conv["launches"]
@@ -296,6 +298,42 @@ def main():
             "launches": conv["launches"],
             "share_of_step": conv["seconds"] / elapsed,
         })
+        if enc_name == "stem_conv_pool":
+            # the fused stem: fp32-class conv on split-bf16 MFMAs + BN/ReLU/pool + codes;
+            # algorithmic work = the reference's fp32 conv MACs, priced against the fp32
+            # peak (the arithmetic the reference runs, 157.3 TFLOP/s MFMA/VALU)
+            n_img = args.batch
+            stem_bytes = n_img * (3 * 224 * 224 * 4 + 64 * 56 * 56 * (4 + 2))
+            roof_tr = {
+                "kernel": "stem_conv_pool_kernel (ResNet stem conv 7x7/2 in fp32 arithmetic on "
+                          "split-bf16 v_mfma_f32_16x16x32_bf16 + BN/ReLU/max-pool + first "
+                          "activation TR -> fp16 codes)",
+                "bound": "mfma",
+                "achieved": 2 * enc_bytes / enc_t / 1e12,
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s (fp32-equivalent)",
+                "frac": 2 * enc_bytes / enc_t / 1e12 / FP32_PEAK_TFLOPS,
+                "hbm_gbs": stem_bytes / enc_t / 1e9,
+                "traffic": enc_traffic,
+                "algorithmic_macs_per_launch": enc_bytes,
+                "avg_launch_us": enc_t * 1e6,
+                "launches": enc["launches"],
+            }
+        else:
+            roof_tr = {
+                "kernel": ("bn_relu_maxpool_encode_kernel (stem BN/ReLU/max-pool + activation "
+                           "TR -> 16-bit codes)" if enc_name == "stem_pool_encode" else
+                           "act_encode_kernel (TR of activations -> 16-bit codes)"),
+                "bound": "hbm",
+                "achieved": enc_bytes / enc_t / 1e9,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": enc_bytes / enc_t / 1e9 / HBM_PEAK_GBS,
+                "traffic": enc_traffic,
+                "algorithmic_bytes_per_launch": enc_bytes,
+                "avg_launch_us": enc_t * 1e6,
+                "launches": enc["launches"],
+            }
         result = {
             "metric": METRIC,
             "value": ips,
@@ -321,20 +359,7 @@ def main():
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,
             "roofline": roof,
-            "roofline_tr": {
-                "kernel": ("bn_relu_maxpool_encode_kernel (stem BN/ReLU/max-pool + activation "
-                           "TR -> 16-bit codes)" if enc_name == "stem_pool_encode" else
-                           "act_encode_kernel (TR of activations -> 16-bit codes)"),
-                "bound": "hbm",
-                "achieved": enc_bytes / enc_t / 1e9,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": enc_bytes / enc_t / 1e9 / HBM_PEAK_GBS,
-                "traffic": enc_traffic,
-                "algorithmic_bytes_per_launch": enc_bytes,
-                "avg_launch_us": enc_t * 1e6,
-                "launches": enc["launches"],
-            },
+            "roofline_tr": roof_tr,
             "accuracy_counters": acc_counters,
         }
         if world == 1 and not args.no_cpu_baseline:

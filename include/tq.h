@@ -224,6 +224,30 @@ int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, i
                               void *stream);
 
 /*
+ * The whole stem of a TQ ResNet in one pass (torchvision ResNet.forward: conv1 -> bn1 -> relu
+ * -> maxpool, then the first TR layers' input TR, tr_layer.py:96-99): conv 7x7 stride 2
+ * pad 3, 3 -> 64 channels, no bias, in fp32 arithmetic on the bf16 matrix cores (three-way
+ * bf16 split of inputs and weights, six partial products per pair; per-product relative
+ * error ~2^-25, the class of the reference's fp32 cuDNN conv), eval BatchNorm
+ * out = conv * scale[c] + shift[c] (fp32 fma), ReLU, max-pool 3x3 stride 2 pad 1, fp32
+ * output and codes as tq_bn_relu_maxpool_encode.  The 64 x (H/2) x (W/2) conv output never
+ * goes to memory.
+ *   x        fp32 channels_last image [n][h][w][3], 8-byte aligned; h, w multiples of 4
+ *   w_split  [3][64][192] bf16 bits: the three splits of the conv weight in space-to-depth
+ *            K order k = ((sy*4 + sx)*2 + sub_r)*6 + sub_c*3 + c for tap (2sy+sub_r-1,
+ *            2sx+sub_c-1), zero where a tap index is -1 (term-quantization_amd/tq_ops.py
+ *            pack_stem_weight)
+ *   out      fp32 [n][h/4][w/4][64] (ho = h/4, wo = w/4)
+ * TQ_ERR_UNSUPPORTED when the image is too wide for one LDS tile (w/4 > ~100).
+ */
+int tq_stem_conv_pool_encode(const float *x, int64_t n, int64_t h, int64_t w,
+                             const uint16_t *w_split, const float *scale, const float *shift,
+                             float *out, int64_t ho, int64_t wo, void *codes_a, int64_t cp_a,
+                             float sf_a, int32_t bits_a, int32_t terms_a, int32_t fmt_a,
+                             void *codes_b, int64_t cp_b, float sf_b, int32_t bits_b,
+                             int32_t terms_b, int32_t fmt_b, void *stream);
+
+/*
  * Batched activation-scale calibration, replacing the 2048-launch loop of
  * tr_layer.mse_profile (tr_layer.py:43-54):
  *   errs[s] = sum_b hist[b] * (x[b] - TR(x[b]; sf = sfs[s], bitwidth, group 1, k))^2

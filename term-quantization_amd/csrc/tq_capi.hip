@@ -376,7 +376,7 @@ int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, i
   if (rc != TQ_OK) return rc;
   if ((codes_a && (uintptr_t)codes_a % 16) || (codes_b && (uintptr_t)codes_b % 16))
     return fail(TQ_ERR_INVALID_ARGUMENT, "bn_relu_maxpool: codes must be 16-byte aligned");
-  tq::PoolArgs a;
+  tq::PoolArgs a = tq::PoolArgs();
   a.x = x;
   a.scale = scale;
   a.shift = shift;
@@ -406,6 +406,60 @@ int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, i
   a.k_b = terms_b < 0 ? 0 : terms_b;
   return hip_status(tq::launch_bn_relu_maxpool_encode(a, (hipStream_t)stream),
                     "bn_relu_maxpool launch");
+}
+
+int tq_stem_conv_pool_encode(const float* x, int64_t n, int64_t h, int64_t w,
+                             const uint16_t* w_split, const float* scale, const float* shift,
+                             float* out, int64_t ho, int64_t wo, void* codes_a, int64_t cp_a,
+                             float sf_a, int32_t bits_a, int32_t terms_a, int32_t fmt_a,
+                             void* codes_b, int64_t cp_b, float sf_b, int32_t bits_b,
+                             int32_t terms_b, int32_t fmt_b, void* stream) {
+  if (n < 0 || h < 4 || w < 4 || h % 4 || w % 4 || ho != h / 4 || wo != w / 4 ||
+      h > (1 << 20) || w > (1 << 20))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "stem_conv_pool: needs H, W % 4 == 0 and Ho = H/4, "
+                                         "Wo = W/4 (conv 7x7/2 pad 3, pool 3x3/2 pad 1)");
+  if (!x || !w_split || !out || !scale || !shift || (uintptr_t)x % 8 ||
+      (uintptr_t)w_split % 16 || (uintptr_t)out % 16)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "stem_conv_pool: null or misaligned buffer");
+  int rc = code_target(codes_a, cp_a, sf_a, bits_a, terms_a, fmt_a, 64, "a");
+  if (rc != TQ_OK) return rc;
+  rc = code_target(codes_b, cp_b, sf_b, bits_b, terms_b, fmt_b, 64, "b");
+  if (rc != TQ_OK) return rc;
+  if ((codes_a && (uintptr_t)codes_a % 16) || (codes_b && (uintptr_t)codes_b % 16))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "stem_conv_pool: codes must be 16-byte aligned");
+  tq::PoolArgs a = tq::PoolArgs();
+  a.x = x;
+  a.wsplit = w_split;
+  a.scale = scale;
+  a.shift = shift;
+  a.out = out;
+  a.N = (int)n;
+  a.H = (int)h;
+  a.W = (int)w;
+  a.C = 64;
+  a.Ho = (int)ho;
+  a.Wo = (int)wo;
+  a.k = 3;
+  a.s = 2;
+  a.pad = 1;
+  a.codes_a = static_cast<int16_t*>(codes_a);
+  a.fmt_a = fmt_a;
+  a.cp_a = (int)cp_a;
+  a.sf_a = sf_a;
+  a.inv_a = 1.0 / (double)sf_a;
+  a.maxv_a = (float)((1u << (codes_a ? bits_a : 0)) - 1u);
+  a.k_a = terms_a < 0 ? 0 : terms_a;
+  a.codes_b = static_cast<int16_t*>(codes_b);
+  a.fmt_b = fmt_b;
+  a.cp_b = (int)cp_b;
+  a.sf_b = sf_b;
+  a.inv_b = 1.0 / (double)sf_b;
+  a.maxv_b = (float)((1u << (codes_b ? bits_b : 0)) - 1u);
+  a.k_b = terms_b < 0 ? 0 : terms_b;
+  const hipError_t e = tq::launch_stem_conv_pool(a, (hipStream_t)stream);
+  if (e == hipErrorInvalidConfiguration)
+    return fail(TQ_ERR_UNSUPPORTED, "stem_conv_pool: image too wide for the LDS tile");
+  return hip_status(e, "stem_conv_pool launch");
 }
 
 int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,

@@ -81,9 +81,13 @@ struct PoolArgs {
   float sf_b, maxv_b;
   int fmt_a, fmt_b;
   double inv_a, inv_b;   // RN64(1 / sf_a), RN64(1 / sf_b)
+  // fused stem (tq_stem_conv.hip): x is the [N][H][W][3] input image, H/W its size, and
+  // wsplit the conv weights as three bf16 splits [3][64][192] (s2d K order)
+  const uint16_t* wsplit;
 };
 
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
+hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream);
 
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
                              int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,

@@ -132,10 +132,42 @@ class FusedResNet(nn.Module):
                            bn.running_mean.detach().double() * a).float().contiguous()
         self.fuse_stem = (self.pool is not None and not bn.training and
                           bn.num_features % 8 == 0)
+        # the whole stem (conv + BN + ReLU + pool + codes) in one kernel when it is the
+        # torchvision shape: conv 7x7/2 pad 3, 3 -> 64, no bias; pool 3x3/2 pad 1
+        c1 = qmodel.conv1
+        self.stem_w = None
+        if (self.fuse_stem and self.pool == (3, 2, 1) and isinstance(c1, nn.Conv2d)
+                and type(c1) is nn.Conv2d and c1.in_channels == 3 and c1.out_channels == 64
+                and c1.kernel_size == (7, 7) and c1.stride == (2, 2) and c1.padding == (3, 3)
+                and c1.dilation == (1, 1) and c1.groups == 1 and c1.bias is None
+                and c1.weight.dtype == torch.float32):
+            self.stem_w = tq_ops.pack_stem_weight(c1.weight)
+
+    def _stem_fused(self, x, first):
+        n, _, h, w = x.shape
+        out = torch.empty((n, 64, h // 4, w // 4), dtype=torch.float32, device=x.device,
+                          memory_format=torch.channels_last)
+        codes = torch.empty((n, h // 4, w // 4, first.conv1.cp_in),
+                            dtype=first.conv1.code_dtype, device=x.device)
+        codes_down = None
+        if first.down is not None:
+            codes_down = torch.empty((n, h // 4, w // 4, first.down.cp_in),
+                                     dtype=first.down.code_dtype, device=x.device)
+        # work = the stem conv's fp32 MACs (7x7x3 per output of the 64 x H/2 x W/2 conv)
+        tq_ops._launch(
+            "stem_conv_pool", n * 64 * (h // 2) * (w // 2) * 147,
+            lambda: tq_native.stem_conv_pool_encode(
+                x, self.stem_w, self.stem_scale, self.stem_shift, out, codes_a=codes,
+                quant_a=first.conv1.quant, codes_b=codes_down,
+                quant_b=first.down.quant if first.down is not None else None))
+        return out, codes, codes_down
 
     def _stem(self, x):
         m = self.qmodel
         first = self.blocks[0]
+        n, _, h, w = x.shape
+        if self.stem_w is not None and h % 4 == 0 and w % 4 == 0 and w // 4 <= 98:
+            return self._stem_fused(x, first)
         if not self.fuse_stem:
             x = m.maxpool(m.relu(m.bn1(m.conv1(x)))).contiguous(
                 memory_format=torch.channels_last)

@@ -67,6 +67,9 @@ _SIGNATURES["tq_conv2d_termpair_fused"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
     _i64, _f64, _vp, _vp, _i64, _i64, ctypes.POINTER(ConvEpilogue), _vp]
 
+_SIGNATURES["tq_stem_conv_pool_encode"] = [
+    _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _i32,
+    _vp, _i64, _f32, _i32, _i32, _i32, _vp]
 _SIGNATURES["tq_conv2d_termpair_f16"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
     _i64, _f64, _vp, _vp, _i64, _i64, _i32, _i32, _i32, ctypes.POINTER(ConvEpilogue), _vp]
@@ -266,6 +269,27 @@ def conv2d_workspace(pixels, cout, device):
     with torch.cuda.device(device):
         nbytes = int(lib().tq_conv2d_workspace_bytes(int(pixels), int(cout)))
     return torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=device)
+
+
+def stem_conv_pool_encode(x, w_split, scale, shift, out, codes_a=None, quant_a=None,
+                          codes_b=None, quant_b=None):
+    """relu(maxpool(bn(conv7x7s2(x)))) of a ResNet stem into ``out`` plus next layers' codes
+    (tq_stem_conv_pool_encode); x fp32 channels_last [N, 3, H, W], w_split from
+    tq_ops.pack_stem_weight."""
+    n, c, h, w = x.shape
+    ho, wo = out.shape[2], out.shape[3]
+    qa = quant_a or (0.0, 0, 0)
+    qb = quant_b or (0.0, 0, 0)
+    with torch.cuda.device(x.device):
+        rc = lib().tq_stem_conv_pool_encode(
+            _ptr(x), n, h, w, _ptr(w_split), _ptr(scale), _ptr(shift), _ptr(out), ho, wo,
+            _ptr(codes_a), codes_a.shape[-1] if codes_a is not None else 0, float(qa[0]),
+            int(qa[1]), int(qa[2]), code_format(codes_a) if codes_a is not None else 0,
+            _ptr(codes_b), codes_b.shape[-1] if codes_b is not None else 0, float(qb[0]),
+            int(qb[1]), int(qb[2]), code_format(codes_b) if codes_b is not None else 0,
+            _stream(x))
+    _check(rc)
+    return out
 
 
 def bn_relu_maxpool_encode(x, scale, shift, k, stride, pad, out, codes_a=None, quant_a=None,

@@ -179,6 +179,25 @@ def mfma_flush_steps(packed, data_bits):
     return 0 if best == s else best
 
 
+def pack_stem_weight(w):
+    """ResNet stem conv weight [64, 3, 7, 7] fp32 -> [3, 64, 192] bf16 bits (int16 tensor) for
+    tq_stem_conv_pool_encode: the 7x7 kernel padded to 8x8 with a leading zero tap, in
+    space-to-depth K order (sy, sx, sub_r, sub_c, c), split exactly into three bf16 parts
+    w = w0 + w1 + w2 + e (each RN(bf16) of the remainder, |e| <= 2^-27 |w|)."""
+    if tuple(w.shape) != (64, 3, 7, 7) or w.dtype != torch.float32:
+        raise RuntimeError("pack_stem_weight: expects a [64, 3, 7, 7] float32 weight")
+    w8 = torch.zeros((64, 3, 8, 8), dtype=torch.float32, device=w.device)
+    w8[:, :, 1:, 1:] = w.detach()
+    # [o, c, sy, sub_r, sx, sub_c] -> [o, sy, sx, sub_r, sub_c, c]
+    k = w8.view(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(64, 192)
+    w0 = k.to(torch.bfloat16)
+    r1 = k - w0.float()
+    w1 = r1.to(torch.bfloat16)
+    r2 = r1 - w1.float()
+    w2 = r2.to(torch.bfloat16)
+    return torch.stack([w0, w1, w2]).contiguous().view(torch.int16)
+
+
 def mfma_flush_chunk(packed, data_bits, cp, ntaps):
     """mfma_flush_steps for kernels that walk K chunk-major (tq.h ``kc_chunk``): the largest
     n such that every window of n consecutive filter taps of one 64-code channel chunk

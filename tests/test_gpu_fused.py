@@ -76,7 +76,13 @@ def test_fused_epilogue_matches_reference_composition(cfg, engine):
     assert torch.equal(got, torch.from_numpy(exp_codes))
 
 
-def test_fused_resnet_matches_module_path(engine):
+@pytest.mark.parametrize("fused_stem", [False, True])
+def test_fused_resnet_matches_module_path(engine, fused_stem):
+    """With the module path's stem (MIOpen fp32 conv) the executors agree to the BN-fold
+    rounding.  The fused stem computes the same fp32-class conv in another summation order;
+    its ~1e-7 differences flip a few activation codes sitting on a quantization boundary,
+    and 17 quantized layers amplify those flips, so that comparison is looser (the stem
+    itself is checked against fp64 in test_gpu_stem.py)."""
     torch.manual_seed(0)
     model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
     settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
@@ -86,11 +92,15 @@ def test_fused_resnet_matches_module_path(engine):
         q(x)
     tr_layer.set_tr_tracking(q, False)
     fused = tq_fuse.FusedResNet(q)
+    if not fused_stem:
+        fused.stem_w = None
+    else:
+        assert fused.stem_w is not None
     with torch.no_grad():
         ref = q(x)
         got = fused(x)
     rel = (got - ref).norm() / ref.norm()
-    assert rel.item() < 1e-3, rel.item()
+    assert rel.item() < (2e-2 if fused_stem else 1e-3), rel.item()
     assert (got.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.75
 
 

@@ -1,0 +1,77 @@
+"""GPU parity of the fused ResNet stem (conv 7x7/2 on split-bf16 matrix cores + BN + ReLU +
+max-pool + first-layer TR codes, tq_stem_conv_pool_encode) against an fp64 reference."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import oracle
+import tq_native
+import tq_ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _bn_coefs(seed):
+    torch.manual_seed(seed)
+    bn = nn.BatchNorm2d(64).eval()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.5, 1.5)  # negative scales: BN must come before the max
+        bn.bias.uniform_(-0.3, 0.3)
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    a = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    return a.float().contiguous(), (bn.bias.double() - bn.running_mean.double() * a).float()
+
+
+@pytest.mark.parametrize("n,h,w,fmt", [(3, 32, 48, torch.float16), (2, 224, 224, torch.float16),
+                                       (1, 64, 36, torch.int16), (2, 20, 392, torch.float16)])
+def test_stem_conv_pool_matches_fp64(n, h, w, fmt):
+    torch.manual_seed(h + w)
+    x = (torch.randn(n, 3, h, w) * 2).contiguous(memory_format=torch.channels_last)
+    wt = torch.empty(64, 3, 7, 7)
+    nn.init.kaiming_normal_(wt, mode="fan_out", nonlinearity="relu")
+    sc, sh = _bn_coefs(h)
+    ho, wo = h // 4, w // 4
+    out = torch.full((n, 64, ho, wo), float("nan"), device=DEV).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.zeros((n, ho, wo, 64), dtype=fmt, device=DEV)
+    wsplit = tq_ops.pack_stem_weight(wt.to(DEV))
+    tq_native.stem_conv_pool_encode(x.to(DEV), wsplit, sc.to(DEV), sh.to(DEV), out,
+                                    codes_a=codes, quant_a=(0.05, 9, 3))
+    got = out.cpu().double()
+    # fp64 reference: conv -> BN (the fp32 coefficients) -> ReLU -> max-pool
+    z = F.conv2d(x.double(), wt.double(), None, 2, 3)
+    mag = F.conv2d(x.double().abs(), wt.double().abs(), None, 2, 3)
+    sd, hd = sc.double().view(1, -1, 1, 1), sh.double().view(1, -1, 1, 1)
+    ref = F.max_pool2d(torch.relu(z * sd + hd), 3, 2, 1)
+    tol = 1e-5 * F.max_pool2d(mag * sd.abs() + hd.abs(), 3, 2, 1) + 1e-30
+    err = (got - ref).abs()
+    assert not torch.isnan(got).any()
+    assert bool((err <= tol).all()), float((err / tol).max())
+    # the codes are exactly TR of the fp32 output the kernel wrote (tr_layer.py:96-99)
+    yq = oracle.tr(out.contiguous().cpu().numpy().reshape(1, -1, 1, 1), 0.05, 9, 1, 3)
+    exp = np.rint(yq.reshape(out.shape) / np.float32(0.05)).astype(np.int64)
+    assert torch.equal(codes.cpu().long().permute(0, 3, 1, 2), torch.from_numpy(exp))
+
+
+def test_stem_split_weights_are_exact_to_2e27():
+    torch.manual_seed(3)
+    wt = torch.randn(64, 3, 7, 7) * 0.1
+    s = tq_ops.pack_stem_weight(wt).view(torch.bfloat16).float()  # [3, 64, 192]
+    tot = (s[0].double() + s[1].double() + s[2].double())
+    w8 = torch.zeros(64, 3, 8, 8, dtype=torch.float64)
+    w8[:, :, 1:, 1:] = wt.double()
+    k = w8.view(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(64, 192)
+    assert bool(((tot - k).abs() <= 2.0**-26 * k.abs()).all())
+
+
+def test_stem_rejects_bad_shapes():
+    x = torch.zeros((1, 3, 30, 32), device=DEV).contiguous(memory_format=torch.channels_last)
+    out = torch.zeros((1, 64, 7, 8), device=DEV).contiguous(memory_format=torch.channels_last)
+    wsplit = tq_ops.pack_stem_weight(torch.zeros(64, 3, 7, 7, device=DEV))
+    sc = torch.ones(64, device=DEV)
+    with pytest.raises(RuntimeError, match="H, W % 4"):
+        tq_native.stem_conv_pool_encode(x, wsplit, sc, sc, out)
