@@ -238,7 +238,7 @@ int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, i
  *            2sx+sub_c-1), zero where a tap index is -1 (term-quantization_amd/tq_ops.py
  *            pack_stem_weight)
  *   out      fp32 [n][h/4][w/4][64] (ho = h/4, wo = w/4)
- * TQ_ERR_UNSUPPORTED when the image is too wide for one LDS tile (w/4 > ~100).
+ * TQ_ERR_UNSUPPORTED when the image is too wide for one LDS tile (w/4 > 84).
  */
 int tq_stem_conv_pool_encode(const float *x, int64_t n, int64_t h, int64_t w,
                              const uint16_t *w_split, const float *scale, const float *shift,

@@ -21,15 +21,19 @@
 // 2R, 2R+1 x cols 2C, 2C+1 x 3 channels = 12 values; conv pixel (oy, ox) reads s2d rows
 // oy-2..oy+1 and cols ox-2..ox+1, so K = 4 x 4 x 12 = 192 in the order (sy, sx, sub_r, sub_c,
 // c), and any 8 consecutive K values are 8 consecutive fp32 in an s2d row ([col][12] rows).
-//   LDS: weights [3 splits][64 rows of 200 bf16] (76.8 KB, staged once per workgroup) and
+//   LDS: weights [3 splits][64 rows of 208 bf16] (80 KB, staged once per workgroup) and
 //        the input tile as fp32 s2d rows [2TP+4][SC][12] (46 KB for TP = 2, W = 224)
-//   wave = one strip of 16 conv columns (7 pool columns) x 2TP+1 conv rows; per conv row
-//        6 K-steps x (4 Cout blocks x 6 split products) v_mfma_f32_16x16x32_bf16
-//   epilogue in registers: BN (fp32 fma, as the stem-tail kernel) + ReLU, vertical max over
-//        the 3 conv rows of each pool row, horizontal max by lane shuffles (width 16),
-//        fp32 store + TR codes for 7 pool pixels per strip.
+//   wave = one strip of 16 conv columns (7 pool columns) x 2TP+1 conv rows, two rows at a
+//        time; per row 6 K-steps x (4 Cout blocks x 6 split products)
+//        v_mfma_f32_16x16x32_bf16, each weight fragment read once for both rows
+//   epilogue: BN (fp32 fma, as the stem-tail kernel) + ReLU, vertical max over the 3 conv
+//        rows of each pool row in registers, horizontal max by lane shuffles (width 16), the
+//        strip's 7 pool pixels x 64 channels compacted through LDS (1.8 KB per wave), then
+//        contiguous fp32 stores + TR codes, every lane finishing 4 channels of <= 2 quads.
 // Max-pool pads with -inf; after ReLU every window holds a valid value >= 0, so the padded
 // conv positions are read as 0 here with the same result.
+#include <type_traits>
+
 #include "tq_device.h"
 #include "tq_launch.h"
 
@@ -43,7 +47,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kStemThreads = 512;
 constexpr int kStemK = 192;     // s2d K
-constexpr int kStemWRow = 200;  // LDS weight row (bf16): 400 B keeps the A reads spread
+constexpr int kStemWRow = 208;  // LDS weight row (bf16): 416 B makes the A reads conflict-free
 constexpr int kStemWBytes = 3 * 64 * kStemWRow * 2;
 
 __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& x0, bf16x8& x1,
@@ -66,6 +70,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   extern __shared__ __attribute__((aligned(16))) u32x4 lds_raw[];
   uint16_t* ws = reinterpret_cast<uint16_t*>(lds_raw);
   float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(lds_raw) + kStemWBytes);
+  // per-wave pool staging: 7 pixels x 64 channels fp32 behind the input rows
+  float* pb = xs + (2 * TP + 4) * sc * 12 + (threadIdx.x >> 6) * (7 * 64);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -91,41 +97,71 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       bsh[mb][i] = a.shift[mb * 16 + 4 * g + i];
     }
 
+  // Input staging, software-pipelined across tiles: the next tile's rows are loaded into
+  // registers while this tile computes, and written to LDS between the two.  Wave w moves
+  // (s2d row, sub row) pairs w, w + 8, ...; lane l float4s l, l + 64, ... of an input row
+  // (3W floats).  The s2d halo columns (input columns outside the image) stay zero.
+  constexpr int ROWS = 2 * (2 * TP + 4);
+  constexpr int RPW = (ROWS + 7) / 8;
+  constexpr int QMAX = 4;  // float4 per lane and row: W <= 340
+  const int f4n = 3 * a.W / 4;
+  for (int i = tid; i < (2 * TP + 4) * sc * 3; i += kStemThreads)
+    reinterpret_cast<float4*>(xs)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 pre[RPW][QMAX];
+  auto prefetch = [&](int t) {
+    const int tn = t / tpi;
+    const int srow0 = 2 * (t - tn * tpi) * TP - 3;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rid = wave + 8 * r;
+      const int ir = 2 * (srow0 + (rid >> 1)) + (rid & 1);
+      const bool rok = rid < ROWS && ir >= 0 && ir < a.H;
+      const float4* src =
+          reinterpret_cast<const float4*>(a.x + ((int64_t)tn * a.H + (rok ? ir : 0)) * a.W * 3);
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q) {
+        const int idx = lane + 64 * q;
+        pre[r][q] = (rok && idx < f4n) ? src[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rid = wave + 8 * r;
+      if (rid >= ROWS) continue;
+      float* row = xs + (rid >> 1) * sc * 12 + (rid & 1) * 6;
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q) {
+        const int idx = lane + 64 * q;
+        if (idx >= f4n) continue;
+        // flat input-row float f -> s2d column 3 + f / 6, slot f % 6 of the sub row
+        const int f = 4 * idx;
+        *reinterpret_cast<float2*>(row + (3 + f / 6) * 12 + f % 6) =
+            make_float2(pre[r][q].x, pre[r][q].y);
+        *reinterpret_cast<float2*>(row + (3 + (f + 2) / 6) * 12 + (f + 2) % 6) =
+            make_float2(pre[r][q].z, pre[r][q].w);
+      }
+    }
+  };
+  if (blockIdx.x < tiles) prefetch(blockIdx.x);
+
   for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int n = tile / tpi;
     const int py0 = (tile - n * tpi) * TP;
-    const int srow0 = 2 * py0 - 3;
-    __syncthreads();  // the previous tile's s2d rows are no longer read
-    // input rows -> s2d: item = (local s2d row, sub row, local s2d col), 6 floats each
-    const int items = (2 * TP + 4) * 2 * sc;
-    for (int it = tid; it < items; it += kStemThreads) {
-      const int lr = it / (2 * sc);
-      const int rem = it - lr * 2 * sc;
-      const int sr = rem / sc;
-      const int lc = rem - sr * sc;
-      const int ir = 2 * (srow0 + lr) + sr;
-      const int ic = 2 * (lc - 3);
-      float2 v0 = make_float2(0.f, 0.f), v1 = v0, v2 = v0;
-      if (ir >= 0 && ir < a.H && ic >= 0 && ic < a.W) {
-        const float* src = a.x + (((int64_t)n * a.H + ir) * a.W + ic) * 3;
-        v0 = *reinterpret_cast<const float2*>(src);
-        v1 = *reinterpret_cast<const float2*>(src + 2);
-        v2 = *reinterpret_cast<const float2*>(src + 4);
-      }
-      float* dst = xs + (lr * sc + lc) * 12 + sr * 6;
-      *reinterpret_cast<float2*>(dst) = v0;
-      *reinterpret_cast<float2*>(dst + 2) = v1;
-      *reinterpret_cast<float2*>(dst + 4) = v2;
-    }
+    __syncthreads();  // the previous tile's s2d rows are no longer read (and xs is zeroed)
+    commit();
     __syncthreads();
+    if (tile + (int)gridDim.x < tiles) prefetch(tile + gridDim.x);
 
     for (int b = wave; b < nb; b += kStemThreads / 64) {
       const int c0 = 14 * b - 1;  // first conv column of the strip
       const int ox = c0 + i16;
       const bool colok = ox >= 0 && ox < Wc;
 
-      // BN + ReLU of conv row (2*py0 - 1 + rr) at column ox, channels mb*16 + 4g + i.
-      // The input slice of step ks+1 is read during step ks's MFMAs.
+      // BN + ReLU of conv rows (2*py0 - 1 + rr + r), r < NR, at column ox, channels
+      // mb*16 + 4g + i.  Rows in pairs share every weight fragment read (LDS traffic), and
+      // the input slices of step ks+1 are read during step ks's MFMAs.
       auto load_x = [&](int rr, int ks, float (&xv)[8]) {
         const int j = 4 * ks + g;  // 8-value K slice of this lane
         const int sy = j / 6;
@@ -136,78 +172,116 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         xv[0] = xa.x; xv[1] = xa.y; xv[2] = xa.z; xv[3] = xa.w;
         xv[4] = xb.x; xv[5] = xb.y; xv[6] = xb.z; xv[7] = xb.w;
       };
-      auto mma_step = [&](int ks, const float (&xv)[8], f32x4 (&acc)[4]) {
-        bf16x8 x0, x1, x2;
-        split3(xv, x0, x1, x2);
+      auto conv_rows = [&](auto nr_tag, int rr, f32x4 (&y)[2][4]) {
+        constexpr int NR = decltype(nr_tag)::value;
+        f32x4 acc[NR][4];
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-          const uint16_t* wr = ws + (mb * 16 + i16) * kStemWRow + 32 * ks + 8 * g;
-          const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(wr);
-          const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(wr + 64 * kStemWRow);
-          const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(wr + 128 * kStemWRow);
-          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x0, acc[mb], 0, 0, 0);
-          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x1, acc[mb], 0, 0, 0);
-          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x0, acc[mb], 0, 0, 0);
-          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x2, acc[mb], 0, 0, 0);
-          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1, acc[mb], 0, 0, 0);
-          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x0, acc[mb], 0, 0, 0);
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) acc[r][mb] = (f32x4)0.0f;
+        float xc[NR][8], xn[NR][8];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) load_x(rr + r, 0, xc[r]);
+#pragma unroll 1
+        for (int ks = 0; ks < kStemK / 32; ++ks) {
+          if (ks + 1 < kStemK / 32) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 1, xn[r]);
+          }
+          bf16x8 x0[NR], x1[NR], x2[NR];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            if (a.ab & 1) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) x0[r][e] = x1[r][e] = x2[r][e] = (__bf16)xc[r][e];
+            } else {
+              split3(xc[r], x0[r], x1[r], x2[r]);
+            }
+          }
+          if (a.ab & 2) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+              acc[r][0][0] += (float)x0[r][0] + (float)x1[r][1] + (float)x2[r][2];
+          } else {
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) {
+            const uint16_t* wr = ws + (mb * 16 + i16) * kStemWRow + 32 * ks + 8 * g;
+            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(wr);
+            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(wr + 64 * kStemWRow);
+            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(wr + 128 * kStemWRow);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              f32x4 c = acc[r][mb];
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x0[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x1[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x0[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x2[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x0[r], c, 0, 0, 0);
+              acc[r][mb] = c;
+            }
+          }
+          }
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xc[r][e] = xn[r][e];
+        }
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int oy = 2 * py0 - 1 + rr + r;
+          const bool ok = colok && oy >= 0 && oy < Hc;
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v = fmaf(acc[r][mb][i], bsc[mb][i], bsh[mb][i]);
+              y[r][mb][i] = ok ? fmaxf(v, 0.0f) : 0.0f;
+            }
         }
       };
-      auto conv_row = [&](int rr, f32x4 (&y)[4]) {
-        f32x4 acc[4];
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) acc[mb] = (f32x4)0.0f;
-        float xa[8], xb[8];
-        load_x(rr, 0, xa);
-#pragma unroll 1
-        for (int ks = 0; ks < kStemK / 32; ks += 2) {
-          load_x(rr, ks + 1, xb);
-          mma_step(ks, xa, acc);
-          if (ks + 2 < kStemK / 32) load_x(rr, ks + 2, xa);
-          mma_step(ks + 1, xb, acc);
-        }
-        const int oy = 2 * py0 - 1 + rr;
-        const bool ok = colok && oy >= 0 && oy < Hc;
+
+      // Pool row j = max over conv rows rr = 2j, 2j+1, 2j+2: rows are computed in pairs
+      // (2i, 2i+1); row 2i closes pool row i-1 and, with row 2i+1, opens pool row i.
+      auto emit_pool = [&](int j, const f32x4 (&run)[4], const f32x4 (&last)[4]) {
+        const int py = py0 + j;
+        float m[4][4];
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float v = fmaf(acc[mb][i], bsc[mb][i], bsh[mb][i]);
-            y[mb][i] = ok ? fmaxf(v, 0.0f) : 0.0f;
-          }
-      };
-
-      // pool row j = max over conv rows rr = 2j, 2j+1, 2j+2 (rows 2j+2 are shared)
-      f32x4 run[4];
-#pragma unroll 1
-      for (int rr = 0; rr <= 2 * TP; ++rr) {
-        f32x4 y[4];
-        conv_row(rr, y);
-        if (rr == 0 || (rr & 1)) {
-#pragma unroll
-          for (int mb = 0; mb < 4; ++mb) run[mb] = rr == 0 ? y[mb] : __builtin_elementwise_max(run[mb], y[mb]);
-          continue;
-        }
-        const int py = py0 + rr / 2 - 1;
-        float m[4][4];
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float v = fmaxf(run[mb][i], y[mb][i]);
+            const float v = fmaxf(run[mb][i], last[mb][i]);
             const float v1 = __shfl_down(v, 1, 16);
             const float v2 = __shfl_down(v, 2, 16);
             m[mb][i] = fmaxf(fmaxf(v, v1), v2);
           }
-          run[mb] = y[mb];
+        // compact the strip's 7 pool pixels x 64 channels through LDS, then every lane
+        // finishes 4 consecutive channels of up to two of the 112 quads: contiguous stores
+        // and no TR work on the 9 lanes of each row that hold no pool output
+        if (py >= a.Ho) return;
+        if (a.ab & 4) {
+          if (m[0][0] == -1.0f) a.out[0] = m[1][1];
+          return;
         }
-        const int px = 7 * b + (i16 >> 1);
-        if (py >= a.Ho || (i16 & 1) || i16 > 12 || px >= a.Wo) continue;
-        const int64_t p = ((int64_t)n * a.Ho + py) * a.Wo + px;
+        const int q = i16 >> 1;
+        if (!(i16 & 1) && i16 <= 12) {
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-          const int co = mb * 16 + 4 * g;
-          const float yv[4] = {m[mb][0], m[mb][1], m[mb][2], m[mb][3]};
+          for (int mb = 0; mb < 4; ++mb)
+            *reinterpret_cast<f32x4*>(pb + q * 64 + mb * 16 + 4 * g) =
+                (f32x4){m[mb][0], m[mb][1], m[mb][2], m[mb][3]};
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the strip is in LDS
+        __builtin_amdgcn_wave_barrier();
+        const int npx = min(7, a.Wo - 7 * b);
+        const int64_t p0 = ((int64_t)n * a.Ho + py) * a.Wo + 7 * b;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int f = lane + 64 * h;  // quad: pixel f / 16, channels 4 (f % 16) .. +3
+          if (f >= 16 * npx) continue;
+          const int co = 4 * (f & 15);
+          const int64_t p = p0 + (f >> 4);
+          const f32x4 v4 = *reinterpret_cast<const f32x4*>(pb + 4 * f);
+          const float yv[4] = {v4[0], v4[1], v4[2], v4[3]};
           *reinterpret_cast<float4*>(a.out + p * 64 + co) =
               make_float4(yv[0], yv[1], yv[2], yv[3]);
 #pragma unroll
@@ -227,16 +301,33 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
                 make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
           }
         }
+        __builtin_amdgcn_wave_barrier();  // pb is rewritten by the next pool row
+      };
+
+      f32x4 run[4];
+      f32x4 y[2][4];
+#pragma unroll 1
+      for (int i = 0; i < TP; ++i) {
+        conv_rows(std::integral_constant<int, 2>(), 2 * i, y);
+        if (i > 0) emit_pool(i - 1, run, y[0]);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[0][mb], y[1][mb]);
       }
+      conv_rows(std::integral_constant<int, 1>(), 2 * TP, y);
+      emit_pool(TP - 1, run, y[0]);
     }
   }
 }
 
 template <int TP>
-hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
+hipError_t launch_stem_tp(const PoolArgs& a_in, hipStream_t stream) {
+  PoolArgs a = a_in;
+  static const char* ab = getenv("TQ_AB");
+  a.ab = ab ? atoi(ab) : 0;
   const int nb = (a.Wo + 6) / 7;
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
-  const int64_t bytes = kStemWBytes + (int64_t)(2 * TP + 4) * sc * 12 * 4;
+  const int64_t bytes =
+      kStemWBytes + (int64_t)(2 * TP + 4) * sc * 12 * 4 + (kStemThreads / 64) * 7 * 64 * 4;
   if (bytes > 160 * 1024) return hipErrorInvalidConfiguration;
   static bool attr_set = false;
   if (!attr_set) {
@@ -261,9 +352,14 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
 
 // Shape contract (checked by the C-ABI layer): 3 input channels, H % 4 == 0, W % 4 == 0,
 // conv 7x7/2 pad 3 -> 64 channels, pool 3x3/2 pad 1 -> Ho = H/4, Wo = W/4, Wo <= 112.
+// Four pool rows per tile when the input tile fits in LDS (W <= 224: 9 conv rows for 4 pool
+// rows), else two (measured 717 vs 793 us for the ResNet-18 bench batch).
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream) {
   static const char* tp = getenv("TQ_STEM_TP");  // A/B override (tools only)
-  if (tp && atoi(tp) == 4) return launch_stem_tp<4>(a, stream);
+  if (!(tp && atoi(tp) == 2)) {
+    const hipError_t e = launch_stem_tp<4>(a, stream);
+    if (e != hipErrorInvalidConfiguration) return e;
+  }
   return launch_stem_tp<2>(a, stream);
 }
 

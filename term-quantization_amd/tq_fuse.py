@@ -166,7 +166,7 @@ class FusedResNet(nn.Module):
         m = self.qmodel
         first = self.blocks[0]
         n, _, h, w = x.shape
-        if self.stem_w is not None and h % 4 == 0 and w % 4 == 0 and w // 4 <= 98:
+        if self.stem_w is not None and h % 4 == 0 and w % 4 == 0 and w // 4 <= 84:
             return self._stem_fused(x, first)
         if not self.fuse_stem:
             x = m.maxpool(m.relu(m.bn1(m.conv1(x)))).contiguous(

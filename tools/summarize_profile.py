@@ -20,13 +20,14 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {
-    "conv2d_tp": "conv2d_tp_kernel",
-    "conv2d_tp_mfma": "conv2d_tp_mfma",
-    "act_encode": "act_encode_kernel",
-    "stem_pool_encode": "bn_relu_maxpool_encode_kernel",
-    "tr_elem": "tr_elem_kernel",
-    "tr_group": "tr_group_kernel",
+KERNELS = {  # summary key -> kernel-name substrings (every MFMA term-pair conv engine)
+    "conv2d_tp": ("conv2d_tp_kernel",),
+    "conv2d_tp_mfma": ("conv2d_tp_mfma", "conv2d_tp_patch", "conv2d_tp_direct"),
+    "act_encode": ("act_encode_kernel",),
+    "stem_pool_encode": ("bn_relu_maxpool_encode_kernel",),
+    "stem_conv_pool": ("stem_conv_pool_kernel",),
+    "tr_elem": ("tr_elem_kernel",),
+    "tr_group": ("tr_group_kernel",),
 }
 
 
@@ -48,14 +49,14 @@ def main(tag):
     fetch = pmc(os.path.join(src, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE")
     write = pmc(os.path.join(src, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE")
     summary = {"tag": tag, "kernels": {}}
-    for key, needle in KERNELS.items():
-        names = [n for n in stats if needle in n]
+    for key, needles in KERNELS.items():
+        names = [n for n in stats if any(nd in n for nd in needles)]
         if not names:
             continue
         calls = sum(int(stats[n]["Calls"]) for n in names)
         total_ns = sum(float(stats[n]["TotalDurationNs"]) for n in names)
-        f = [v for n in fetch if needle in n for v in fetch[n]]
-        w = [v for n in write if needle in n for v in write[n]]
+        f = [v for n in fetch if any(nd in n for nd in needles) for v in fetch[n]]
+        w = [v for n in write if any(nd in n for nd in needles) for v in write[n]]
         entry = {"variants": names, "calls": calls, "avg_duration_us": total_ns / calls / 1e3}
         if f and w:
             entry["fetch_bytes_per_launch"] = 2.0 * sum(f) / len(f) * 1024
@@ -72,12 +73,14 @@ def main(tag):
     conv_m = summary["kernels"].get("conv2d_tp_mfma", {})
     enc = summary["kernels"].get("act_encode", {})
     stem = summary["kernels"].get("stem_pool_encode", {})
+    stem_conv = summary["kernels"].get("stem_conv_pool", {})
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as fp:
         json.dump({"source": "profiles/%s_summary.json" % tag,
                    "conv2d_tp_bytes_per_launch": conv.get("hbm_bytes_per_launch"),
                    "conv2d_tp_mfma_bytes_per_launch": conv_m.get("hbm_bytes_per_launch"),
                    "act_encode_bytes_per_launch": enc.get("hbm_bytes_per_launch"),
-                   "stem_pool_encode_bytes_per_launch": stem.get("hbm_bytes_per_launch")}, fp,
+                   "stem_pool_encode_bytes_per_launch": stem.get("hbm_bytes_per_launch"),
+                   "stem_conv_pool_bytes_per_launch": stem_conv.get("hbm_bytes_per_launch")}, fp,
                   indent=1)
     for k, v in summary["kernels"].items():
         print(k, {a: b for a, b in v.items() if a != "variants"})
