@@ -70,25 +70,25 @@ __device__ __forceinline__ void glds16(const void* src, u32x4* lds_wave_base) {
 #define TQ_WAIT_VM(n) \
   __builtin_amdgcn_s_waitcnt(((n) & 15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14))
 
-// s_waitcnt vmcnt(n) for a runtime n: counts above 15 wait for 15 (stricter, still correct).
+// s_waitcnt vmcnt(n) for a runtime n in [0, 63] (larger n waits for 63: stricter, correct).
+template <int N>
+__device__ __forceinline__ void wait_vm_upto(int n) {
+  if constexpr (N < 0) {
+    TQ_WAIT_VM(0);
+  } else {
+    if (n >= N) {
+      TQ_WAIT_VM(N);
+    } else {
+      wait_vm_upto<N - 1>(n);
+    }
+  }
+}
+
 __device__ __forceinline__ void wait_vm_dyn(int n) {
-  switch (n) {
-    case 0: TQ_WAIT_VM(0); break;
-    case 1: TQ_WAIT_VM(1); break;
-    case 2: TQ_WAIT_VM(2); break;
-    case 3: TQ_WAIT_VM(3); break;
-    case 4: TQ_WAIT_VM(4); break;
-    case 5: TQ_WAIT_VM(5); break;
-    case 6: TQ_WAIT_VM(6); break;
-    case 7: TQ_WAIT_VM(7); break;
-    case 8: TQ_WAIT_VM(8); break;
-    case 9: TQ_WAIT_VM(9); break;
-    case 10: TQ_WAIT_VM(10); break;
-    case 11: TQ_WAIT_VM(11); break;
-    case 12: TQ_WAIT_VM(12); break;
-    case 13: TQ_WAIT_VM(13); break;
-    case 14: TQ_WAIT_VM(14); break;
-    default: TQ_WAIT_VM(15); break;
+  if (n >= 15) {
+    wait_vm_upto<63>(n);
+  } else {
+    wait_vm_upto<15>(n);
   }
 }
 

@@ -25,6 +25,8 @@
 //   epilogue: every residual load of the wave tile issued first, then the int32 tile is
 //             transposed through LDS so 16 lanes cover one pixel's 64 channels: each store
 //             instruction writes 4 whole pixel rows (fp32 out: 1 KB, codes: 512 B).
+#include <utility>
+
 #include "tq_device.h"
 #include "tq_epilogue.h"
 #include "tq_launch.h"
@@ -34,23 +36,29 @@ namespace tq {
 
 namespace {
 
+// f(integral_constant<int, J>) for J = 0 .. N-1, unrolled (constant register-array indices)
+template <typename F, int... J>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>()), ...);
+}
+
 constexpr int kDirThreads = 256;
 constexpr int kDirBM = 64;
-constexpr int kDirSlots = 3;  // A ring depth = K-steps in flight + 1
-
-template <int WN>
+// D = K-steps in flight (loads issued ahead of the step being multiplied)
+template <int WN, int D>
 struct DirCfg {
   static constexpr int BN = 4 * 32 * WN;
+  static constexpr int NB = D + 1;                 // B register buffers = A ring slots
   static constexpr int SLOT = kDirBM * 8;          // u32x4 per A slot (64 rows x 128 B)
   static constexpr int TILE = 64 * 32 * WN / 4;    // u32x4 per wave epilogue tile (int32)
-  static constexpr int LDS = kDirSlots * SLOT > 4 * TILE ? kDirSlots * SLOT : 4 * TILE;
+  static constexpr int LDS = NB * SLOT > 4 * TILE ? NB * SLOT : 4 * TILE;
   static constexpr int LPS = 2 + 4 * WN;           // vmem instructions per wave and K-step
 };
 
-template <int WN, bool FLUSH>
+template <int WN, bool FLUSH, int D>
 __global__ __launch_bounds__(kDirThreads, WN == 1 ? 2 : 1) void conv2d_tp_direct_kernel(
     ConvArgs a) {
-  using C = DirCfg<WN>;
+  using C = DirCfg<WN, D>;
   __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
   __shared__ double coef[kDirBM][2];  // epilogue (scale, shift) of the tile's channels
 
@@ -177,26 +185,33 @@ __global__ __launch_bounds__(kDirThreads, WN == 1 ? 2 : 1) void conv2d_tp_direct
     }
   };
 
-  // Two K-steps in flight: step s is retired by vmcnt(LPS) (only step s + 1 younger), a
-  // barrier makes every wave's A-DMA of step s visible and frees slot (s + 2) % 3.
-  u32x4 b0[WN][4], b1[WN][4], b2[WN][4];
-  auto step = [&](int s, int slot, const u32x4 (&bc)[WN][4], u32x4 (&bnext)[WN][4]) {
-    if (s + 1 < nsteps) TQ_WAIT_VM(C::LPS);
-    else TQ_WAIT_VM(0);
+  // D K-steps in flight: step t is retired by vmcnt(LPS * younger) (the loads of the
+  // min(D - 1, nsteps - 1 - t) later steps stay in flight), a barrier makes every wave's
+  // A-DMA of step t visible and frees the slot of step t - 1 for step t + D.
+  u32x4 bufs[C::NB][WN][4];
+  auto step = [&](int t, auto j_tag) {
+    constexpr int j = decltype(j_tag)::value;  // t % NB
+    const int younger = min(D - 1, nsteps - 1 - t);
+    if (younger == D - 1)
+      TQ_WAIT_VM(C::LPS * (D - 1));
+    else
+      wait_vm_dyn(C::LPS * younger);
     __builtin_amdgcn_s_barrier();
-    if (s + 2 < nsteps) issue((slot + 2) % kDirSlots, bnext);
-    compute(slot, bc);
+    if (t + D < nsteps) issue((j + D) % C::NB, bufs[(j + D) % C::NB]);
+    compute(j, bufs[j]);
   };
-  issue(0, b0);
-  if (nsteps > 1) issue(1, b1);
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nsteps) issue(j, bufs[j]);
   int s = 0;
-  for (; s + 2 < nsteps; s += 3) {
-    step(s, 0, b0, b2);
-    step(s + 1, 1, b1, b0);
-    step(s + 2, 2, b2, b1);
-  }
-  if (s < nsteps) step(s, 0, b0, b2);
-  if (s + 1 < nsteps) step(s + 1, 1, b1, b0);
+  for (; s + C::NB <= nsteps; s += C::NB)
+    unroll_seq([&](auto jt) { step(s + decltype(jt)::value, jt); },
+               std::make_integer_sequence<int, C::NB>());
+  unroll_seq(
+      [&](auto jt) {
+        if (s + decltype(jt)::value < nsteps) step(s + decltype(jt)::value, jt);
+      },
+      std::make_integer_sequence<int, C::NB>());
   acc_flush(acc);
 
   // Epilogue.  Lane (slot = lane & 15) finishes channels m0 + 4*slot .. +3 of pixels
@@ -252,12 +267,19 @@ __global__ __launch_bounds__(kDirThreads, WN == 1 ? 2 : 1) void conv2d_tp_direct
   }
 }
 
-template <int WN, bool FLUSH>
+template <int WN, bool FLUSH, int D>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
-  constexpr int BN = DirCfg<WN>::BN;
+  constexpr int BN = DirCfg<WN, D>::BN;
   const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + kDirBM - 1) / kDirBM);
-  conv2d_tp_direct_kernel<WN, FLUSH><<<dim3((unsigned)tiles), kDirThreads, 0, stream>>>(a);
+  conv2d_tp_direct_kernel<WN, FLUSH, D><<<dim3((unsigned)tiles), kDirThreads, 0, stream>>>(a);
   return hipGetLastError();
+}
+
+template <int WN, bool FLUSH>
+hipError_t launch_direct_d(const ConvArgs& a, hipStream_t stream) {
+  if (a.ab & 8) return launch_direct_cfg<WN, FLUSH, 3>(a, stream);   // A/B (tools only)
+  if (a.ab & 16) return launch_direct_cfg<WN, FLUSH, 4>(a, stream);
+  return launch_direct_cfg<WN, FLUSH, 2>(a, stream);
 }
 
 }  // namespace
@@ -270,8 +292,8 @@ bool conv_direct_eligible(const ConvArgs& a, int out_nhwc) {
 hipError_t launch_conv2d_direct(const ConvArgs& a, int wn, hipStream_t stream) {
   const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
   if (wn == 1)
-    return flush ? launch_direct_cfg<1, true>(a, stream) : launch_direct_cfg<1, false>(a, stream);
-  return flush ? launch_direct_cfg<2, true>(a, stream) : launch_direct_cfg<2, false>(a, stream);
+    return flush ? launch_direct_d<1, true>(a, stream) : launch_direct_d<1, false>(a, stream);
+  return flush ? launch_direct_d<2, true>(a, stream) : launch_direct_d<2, false>(a, stream);
 }
 
 }  // namespace tq
