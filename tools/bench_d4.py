@@ -1,0 +1,107 @@
+"""the other configs of BASELINE.json on one MI355X, one JSON line each.
+
+    python tools/bench_d4.py [--steps 10]
+
+* LSTM-650 Wikitext-2 TQ (g=8, k=12, wb=db=dt=8), eval batch 10, bptt 35: random-init
+  RNNModel and uniform random token ids (the WikiText-2 train split that defines the
+  vocabulary is not available offline; the vocabulary size 33,278 is kept).  tokens/s of the
+  TQ forward (TR'd LSTM weights + quantized inputs/hidden state at chunk boundaries, the
+  reference's TRLSTMLayer semantics) and term-pair MACs/s with the decoder count of
+  profile_model (as published).
+* MobileNet-V2 / EfficientNet-b0 TQ (depthwise layers at wb=16, g=1, k=16 as
+  cnn_models.static_conv_layer_settings sets them; other layers g=8, k=12, wb=db=9, dt=3),
+  synthetic N(0,1) 256x3x224x224, random-init weights: images/s of the converted module path
+  (term-pair and depthwise term-pair kernels, torch BN/activations).
+Timing: W untimed warmup steps, then K steps between synchronize calls."""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
+
+import cnn_models  # noqa: E402
+import evaluate_lstm  # noqa: E402
+import profile_model  # noqa: E402
+import tr_layer  # noqa: E402
+from lstm_models import model as model_mod  # noqa: E402
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def lstm(args, dev):
+    torch.manual_seed(1111)
+    ntokens, bsz, bptt = evaluate_lstm.WT2_VOCAB, 10, 35
+    model = model_mod.RNNModel("LSTM", ntokens, 650, 650, 2, 0.5, True).to(dev).eval()
+    tr_params = evaluate_lstm.static_lstm_layer_settings(model, 8, 8, 12)
+    q = evaluate_lstm.convert_model(model, tr_params, 8, 8)
+    tokens = torch.randint(0, ntokens, (bptt * bsz * 4 + bsz,))
+    data = evaluate_lstm.batchify(tokens, bsz, dev)
+    x = evaluate_lstm.get_batch(data, 0, bptt)[0]
+    with torch.no_grad():
+        q(x, model.init_hidden(bsz))  # calibration pass
+        tr_layer.set_tr_tracking(q, False)
+        tmacs, _ = profile_model.get_model_ops(q, inputs=(x, model.init_hidden(bsz)))
+        hidden = model.init_hidden(bsz)
+        t = timed(lambda: q(x, hidden), args.steps, args.warmup)
+    toks = bptt * bsz
+    return {"metric": "LSTM-650 TQ tokens/s", "value": toks / t, "unit": "tokens/s",
+            "ms_per_step": t * 1e3, "term_pair_macs_per_step": tmacs,
+            "term_pair_macs_per_s": tmacs / t,
+            "config": {"workload": "lstm-650 wikitext-2 vocab, g=8 k=12 wb=db=dt=8",
+                       "batch": bsz, "bptt": bptt, "data": "synthetic token ids"}}
+
+
+def cnn(arch, args, dev):
+    torch.manual_seed(0)
+    model = getattr(cnn_models, arch)(pretrained=False).to(dev).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(args.batch, 3, 224, 224, device=dev).contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        tmacs, _ = profile_model.get_model_ops(q, (torch.randn(1, 3, 224, 224, device=dev),))
+        q(x)
+        tr_layer.set_tr_tracking(q, False)
+        t = timed(lambda: q(x), args.steps, args.warmup)
+    modes = sorted({m.mode for m in q.modules() if isinstance(m, tr_layer.TRConv2dLayer)})
+    return {"metric": "%s TQ images/s" % arch, "value": args.batch / t, "unit": "images/s",
+            "ms_per_step": t * 1e3, "term_pair_macs_per_image": tmacs,
+            "term_pair_macs_per_s": tmacs * args.batch / t,
+            "config": {"workload": "%s-tq (dw wb=16 g=1 k=16; others g=8 k=12 wb=db=9 dt=3)"
+                                   % arch, "batch": args.batch, "layer_modes": modes,
+                       "data": "synthetic N(0,1), random-init weights"}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.backends.cudnn.benchmark = True
+    for fn in (lambda: lstm(args, dev), lambda: cnn("mobilenet_v2", args, dev),
+               lambda: cnn("efficientnet_b0", args, dev)):
+        r = fn()
+        if not math.isfinite(r["value"]):
+            raise RuntimeError("non-finite result")
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
