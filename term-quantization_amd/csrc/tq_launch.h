@@ -108,8 +108,9 @@ int conv_mfma_num_configs();
 // MFMA input-patch engine (tr_conv_patch.hip): stride-1 convs with Cp % 64 == 0, NHWC out.
 bool conv_patch_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_patch(const ConvArgs& a, int mb, hipStream_t stream);
-// MFMA direct engine (tr_conv_direct.hip): Cp % 64 == 0, NHWC out; wn = 1 or 2.
+// MFMA direct engine (tr_conv_direct.hip): Cp % 64 == 0, NHWC out; mb = 1 (64 x 128 tiles)
+// or 2 (128 x 128 tiles).
 bool conv_direct_eligible(const ConvArgs& a, int out_nhwc);
-hipError_t launch_conv2d_direct(const ConvArgs& a, int wn, hipStream_t stream);
+hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream);
 
 }  // namespace tq

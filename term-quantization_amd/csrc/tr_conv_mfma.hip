@@ -462,7 +462,7 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // Configs (1-based through ConvArgs.config): 1-2 register-staged (any Cp), 3-6 pipelined
 // gather (Cp % 64 == 0 and KH*KW <= 64; else 1/2), 7-8 input patch (tr_conv_patch.hip:
 // stride 1, KH*KW >= 2, NHWC out; else the gather default).
-// 9-10 direct (tr_conv_direct.hip: Cp % 64 == 0, NHWC out; 256- / 128-pixel tiles).
+// 9-10 direct (tr_conv_direct.hip: Cp % 64 == 0, NHWC out; 128 x 128 / 64 x 128 tiles).
 int conv_mfma_num_configs() { return 10; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
@@ -476,7 +476,7 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   int cfg = a.config > 0 ? a.config - 1 : -1;
   static const char* ab = getenv("TQ_AB");
   a.ab = ab ? atoi(ab) : 0;
-  static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 WN
+  static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 MB
   if (cfg < 0 && dir && atoi(dir) > 0) cfg = atoi(dir) == 1 ? 9 : 8;
   // measured (tools/layer_times.py, ResNet-18 batch 256): the direct engine wins where the
   // fused epilogue dominates -- Cout <= 128 (layer1/2) and 1x1 convs
