@@ -84,7 +84,6 @@ struct PoolArgs {
   // fused stem (tq_stem_conv.hip): x is the [N][H][W][3] input image, H/W its size, and
   // wsplit the conv weights as three bf16 splits [3][64][192] (s2d K order)
   const uint16_t* wsplit;
-  int ab;  // timing-only A/B switches (TQ_AB, tools only; 0 in the product)
 };
 
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);

@@ -190,19 +190,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           }
           bf16x8 x0[NR], x1[NR], x2[NR];
 #pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            if (a.ab & 1) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) x0[r][e] = x1[r][e] = x2[r][e] = (__bf16)xc[r][e];
-            } else {
-              split3(xc[r], x0[r], x1[r], x2[r]);
-            }
-          }
-          if (a.ab & 2) {
-#pragma unroll
-            for (int r = 0; r < NR; ++r)
-              acc[r][0][0] += (float)x0[r][0] + (float)x1[r][1] + (float)x2[r][2];
-          } else {
+          for (int r = 0; r < NR; ++r) split3(xc[r], x0[r], x1[r], x2[r]);
+          {
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) {
             const uint16_t* wr = ws + (mb * 16 + i16) * kStemWRow + 32 * ks + 8 * g;
@@ -259,10 +248,6 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         // finishes 4 consecutive channels of up to two of the 112 quads: contiguous stores
         // and no TR work on the 9 lanes of each row that hold no pool output
         if (py >= a.Ho) return;
-        if (a.ab & 4) {
-          if (m[0][0] == -1.0f) a.out[0] = m[1][1];
-          return;
-        }
         const int q = i16 >> 1;
         if (!(i16 & 1) && i16 <= 12) {
 #pragma unroll
@@ -320,10 +305,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 }
 
 template <int TP>
-hipError_t launch_stem_tp(const PoolArgs& a_in, hipStream_t stream) {
-  PoolArgs a = a_in;
-  static const char* ab = getenv("TQ_AB");
-  a.ab = ab ? atoi(ab) : 0;
+hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   const int nb = (a.Wo + 6) / 7;
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
   const int64_t bytes =
