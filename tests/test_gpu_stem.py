@@ -57,17 +57,6 @@ def test_stem_conv_pool_matches_fp64(n, h, w, fmt):
     assert torch.equal(codes.cpu().long().permute(0, 3, 1, 2), torch.from_numpy(exp))
 
 
-def test_stem_split_weights_are_exact_to_2e27():
-    torch.manual_seed(3)
-    wt = torch.randn(64, 3, 7, 7) * 0.1
-    s = tq_ops.pack_stem_weight(wt).view(torch.bfloat16).float()  # [3, 64, 192]
-    tot = (s[0].double() + s[1].double() + s[2].double())
-    w8 = torch.zeros(64, 3, 8, 8, dtype=torch.float64)
-    w8[:, :, 1:, 1:] = wt.double()
-    k = w8.view(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(64, 192)
-    assert bool(((tot - k).abs() <= 2.0**-26 * k.abs()).all())
-
-
 def test_stem_rejects_bad_shapes():
     x = torch.zeros((1, 3, 30, 32), device=DEV).contiguous(memory_format=torch.channels_last)
     out = torch.zeros((1, 64, 7, 8), device=DEV).contiguous(memory_format=torch.channels_last)

@@ -276,3 +276,55 @@ def test_mfma_flush_steps_bounds():
     small = torch.ones((4, 64, 3, 3), dtype=torch.int32)
     packed, _ = tq_ops.pack_conv_weight(small, "mfma")
     assert tq_ops.mfma_flush_steps(packed, 9) == 0
+
+
+def test_mfma_flush_chunk_windows_cover_chunk_major_order():
+    """kc_chunk (tq_ops.mfma_flush_chunk) bounds every window of consecutive taps of one
+    64-channel chunk -- the order the input-patch engine walks -- and a brute-force walk of
+    that order with flushes every kc_chunk steps and at chunk ends never exceeds 2^24."""
+    import tq_ops  # noqa: F811
+    torch.manual_seed(3)
+    cin, kh = 256, 3
+    codes = torch.randint(-256, 257, (8, cin, kh, kh), dtype=torch.int32)
+    codes[:, :64] *= 0  # uneven chunks: the bound must hold per chunk
+    packed, cp = tq_ops.pack_conv_weight(codes, "mfma")
+    for db in (8, 9):
+        kc = tq_ops.mfma_flush_chunk(packed, db, cp, kh * kh)
+        assert kc >= 1
+        nch = cp // 64
+        steps = packed.double().abs().view(packed.shape[0], -1, 64).sum(-1)  # [O, S]
+        lim = 2.0**24 / 2**db
+        for c in range(nch):
+            seq = [steps[:, t * nch + c] for t in range(kh * kh)]
+            win = torch.zeros(packed.shape[0], dtype=torch.float64)
+            for i, v in enumerate(seq):
+                if i % kc == 0:
+                    win.zero_()
+                win += v
+                assert float(win.max()) <= lim
+        # one step more would break some window (kc is the largest valid one), unless kc
+        # already covers a whole chunk
+        if kc < kh * kh:
+            assert tq_ops.mfma_flush_chunk(packed, db + 1, cp, kh * kh) <= kc
+    assert tq_ops.mfma_flush_chunk(packed[:, :64 * 9], 9, 48, 9) == -1  # Cp % 64 != 0
+
+
+def test_stem_weight_split_is_exact():
+    """pack_stem_weight: three bf16 parts summing to the fp32 weight within 2^-26 relative, in
+    the space-to-depth K order of the stem kernel (zero taps where the 8x8 pad is)."""
+    import tq_ops  # noqa: F811
+    torch.manual_seed(4)
+    w = torch.randn(64, 3, 7, 7) * 0.07
+    parts = tq_ops.pack_stem_weight(w).view(torch.bfloat16).double()  # [3, 64, 192]
+    tot = parts.sum(0)
+    w8 = torch.zeros(64, 3, 8, 8, dtype=torch.float64)
+    w8[:, :, 1:, 1:] = w.double()
+    k = w8.view(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(64, 192)
+    assert bool(((tot - k).abs() <= 2.0**-26 * k.abs()).all())
+    # K index k = ((sy*4 + sx)*2 + sub_r)*6 + sub_c*3 + c  <->  tap (2sy+sub_r-1, 2sx+sub_c-1)
+    for (o, c, r, q) in [(0, 0, 0, 0), (5, 2, 6, 6), (63, 1, 3, 4)]:
+        kh8, kw8 = r + 1, q + 1
+        idx = ((kh8 // 2 * 4 + kw8 // 2) * 2 + kh8 % 2) * 6 + (kw8 % 2) * 3 + c
+        assert abs(float(tot[o, idx]) - float(w[o, c, r, q])) <= 2.0**-26 * abs(float(w[o, c, r, q]))
+    with pytest.raises(RuntimeError):
+        tq_ops.pack_stem_weight(torch.zeros(64, 3, 5, 5))
