@@ -177,8 +177,11 @@ int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int
  *   w_codes    [cout_pad][kp] fp16 codes, cout_pad a multiple of tq_conv2d_cout_align(),
  *              kp a multiple of 64
  * epi == NULL: out = fp32(acc * scale) + bias, NCHW (out_nhwc = 0) or NHWC (out_nhwc = 1).
- * epi != NULL: the fused epilogue of tq_conv2d_termpair_fused (out_nhwc must be 1; its
- * split_k must be 0 or 1: the MFMA engine runs data-parallel tiles).
+ * epi != NULL: the fused epilogue of tq_conv2d_termpair_fused (out_nhwc must be 1).  Its
+ * split_k: 0 = built-in choice, 1 = data-parallel tiles, -1 = stream-K where the engine has
+ * it (the input-patch engine: tiles x K-steps shared evenly by one workgroup per CU, split
+ * tiles finished by their last-arriving piece from int32 slabs -- bit-identical results;
+ * needs `workspace` >= tq_conv2d_workspace_bytes, else data-parallel).
  */
 int32_t tq_conv2d_mfma_num_configs(void);
 

@@ -304,8 +304,8 @@ int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int6
   } else {
     if (!out_nhwc)
       return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_f16: the fused epilogue is channels_last");
-    if (epi->split_k != 0 && epi->split_k != 1)
-      return fail(TQ_ERR_UNSUPPORTED, "conv2d_f16: the MFMA engine does not split K");
+    if (epi->split_k != 0 && epi->split_k != 1 && epi->split_k != -1)
+      return fail(TQ_ERR_UNSUPPORTED, "conv2d_f16: split_k must be 0, 1 or -1");
     rc = apply_epilogue(epi, cout, out, tq::conv_mfma_num_configs(), &a);
     if (rc != TQ_OK) return rc;
   }

@@ -96,6 +96,9 @@ hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, 
 int conv_tile_m(int64_t cout);
 int conv_num_configs();
 int64_t conv_workspace_bytes(int64_t p, int64_t cout);
+int device_cus();  // CUs of the current device (cached per thread)
+// stream-K patch engine: slab + tile-counter bytes it needs in ConvArgs.ws
+int64_t patch_streamk_ws_bytes(int64_t p, int64_t cout);
 
 hipError_t launch_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                               int64_t nsf, int bitwidth, int k, double* errs, hipStream_t stream);

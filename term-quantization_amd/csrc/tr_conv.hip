@@ -449,8 +449,6 @@ int conv_tile_m(int64_t cout) { return cout <= 64 ? 64 : 128; }
 
 int conv_num_configs() { return kNumTileCfgs; }
 
-namespace {
-
 int device_cus() {
   static thread_local int cached_dev = -1, cached_cus = 0;
   int dev = 0;
@@ -465,6 +463,8 @@ int device_cus() {
   }
   return cached_cus;
 }
+
+namespace {
 
 // Resident blocks per CU of the stream-K kernel of one config (occupancy query, cached).
 template <int BM, int BN, int T, int OCC>
@@ -552,7 +552,9 @@ int64_t conv_workspace_bytes(int64_t p, int64_t cout) {
     if (b > sk) sk = b;
   }
   const int64_t split = p * cout * 4;
-  return sk > split ? sk : split;
+  const int64_t r = sk > split ? sk : split;
+  const int64_t ps = patch_streamk_ws_bytes(p, cout);
+  return r > ps ? r : ps;
 }
 
 hipError_t launch_conv2d_tp(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {

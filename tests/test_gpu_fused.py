@@ -164,6 +164,52 @@ def test_schedules_are_bit_identical(layer, cfgs, monkeypatch):
         assert torch.equal(o, o0) and torch.equal(c, c0)
 
 
+@pytest.mark.parametrize("layer,batch", [(8, 5), (13, 8), (13, 37), (16, 8), (19, 3)])
+@pytest.mark.parametrize("cfg", [0, 7, 8])
+def test_patch_streamk_bit_identical(layer, batch, cfg):
+    """The input-patch engine's stream-K schedule (split_k=-1: K-step ranges cut across tile
+    boundaries, split tiles finished from int32 slabs by their last piece) sums the same
+    integers as its data-parallel tiles (split_k=1): outputs and codes bit-identical,
+    including ranges that start inside a channel chunk and batches with fewer K-steps than
+    workgroups (empty ranges)."""
+    import tq_ops
+    from conftest import RESNET18_TR
+    cin, cout, k, s, hin = RESNET18_TR[layer - 1]
+    assert s == 1 and k == 3
+    torch.manual_seed(100 + layer)
+    conv = nn.Conv2d(cin, cout, k, s, 1, bias=False).to(DEV)
+    lay = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    assert lay.engine == "mfma"
+    cp = tq_ops.act_channels(cin)
+    x = torch.relu(torch.randn(batch, cin, hin, hin, device=DEV)).to(
+        memory_format=torch.channels_last)
+    codes = torch.empty((batch, hin, hin, cp), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    ws = tq_native.conv2d_workspace(batch * hin * hin, cout, DEV)
+    sc = torch.rand(cout, dtype=torch.float64, device=DEV) * 1e-4
+    sh = torch.randn(cout, dtype=torch.float64, device=DEV)
+    res = torch.randn(batch, cout, hin, hin, device=DEV).contiguous(
+        memory_format=torch.channels_last)
+    outs = []
+    for sp in (1, -1, -1):  # twice: the counters must be usable again
+        o = torch.full((batch, cout, hin, hin), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.zeros((batch, hin, hin, tq_ops.act_channels(cout)), dtype=torch.float16,
+                         device=DEV)
+        ws.fill_(-7)  # stale slabs/counters must not leak into the sums
+        tq_native.conv2d_termpair_fused(codes, lay.w_codes, cout, k, k, (1, 1), (1, 1),
+                                        (1, 1), hin, hin, out=o, ch_scale=sc, ch_shift=sh,
+                                        residual=res, relu=True, codes_a=ca,
+                                        quant_a=(0.05, 9, 3), workspace=ws, split_k=sp,
+                                        config=cfg, kc_steps=lay.kc_steps,
+                                        kc_chunk=lay.kc_chunk)
+        outs.append((o.cpu(), ca.cpu()))
+    o0, c0 = outs[0]
+    assert not torch.isnan(o0).any()
+    for o, c in outs[1:]:
+        assert torch.equal(o, o0) and torch.equal(c, c0)
+
+
 @pytest.mark.parametrize("dtype", [torch.int16, torch.float16])
 def test_stem_bn_relu_maxpool_encode(dtype):
     torch.manual_seed(11)
