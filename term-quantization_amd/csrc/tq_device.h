@@ -81,6 +81,12 @@ __device__ __forceinline__ uint32_t keep_top_terms(uint32_t mask, int k) {
   return mask;
 }
 
+// Largest HESE term count of a bw-bit magnitude: floor(2 (bw + 1) / 3) -- runs "11" followed
+// by one zero give two terms per three bits (brute-forced for bw <= 20 in
+// tests/test_host.py::test_hese_max_terms).  Peeling the top set bit that many times empties
+// any mask, so the fast path below caps its peel count there.
+__host__ __device__ constexpr int hese_max_terms(int bw) { return 2 * (bw + 1) / 3; }
+
 // a4 -- value of the kept terms, with the element's sign: kernels/tr_cuda_kernel.cu:112.
 __device__ __forceinline__ int32_t kept_value(uint32_t pos, uint32_t neg, uint32_t keep,
                                               bool negative) {
@@ -106,6 +112,46 @@ __device__ __forceinline__ int32_t tr_value_g1_inv(float x, double inv_sf, float
   return tr_value_of_q(quantize_mag_inv(x, inv_sf, maxv), k, x < 0.0f);
 }
 
+// Epilogue fast path for 4 values the epilogue has just passed through ReLU (y >= 0, never
+// NaN) with a finite inv_sf (sf > 0): no sign, no NaN test, and the a1 rounding as
+//   q = cvt(min(r, maxv)) + (fract(min(r, maxv)) >= 0.5)
+// (exact: floor(r + 0.5) = floor(r) + (r - floor(r) >= 0.5); the clamp keeps +inf out of
+// fract, and at the clamp fract(maxv) = 0 since maxv is an integer).  Top-k selection
+// without popcount or a divergent loop: peel the highest set bit npeel times (wave-uniform:
+// one scalar loop for all 4 values, 3 VALU per peel) and keep what was peeled; once a mask
+// is empty its find-first-bit-high is 0xffffffff and the peel clears bit 0 of 0, a no-op.  v[i] == tr_value_g1_inv(y[i], inv_sf, maxv, k) for
+// npeel = min(k, hese_max_terms(bw)).
+__device__ __forceinline__ void tr_values_relu4(const float y[4], double inv_sf, float maxv,
+                                                int npeel, int32_t v[4]) {
+  uint32_t pos[4], neg[4], rest[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float r = fminf(quotient_f32(y[i], inv_sf), maxv);
+    const uint32_t q = (uint32_t)r + (__builtin_amdgcn_fractf(r) >= 0.5f ? 1u : 0u);
+    hese_masks(q, pos[i], neg[i]);
+    rest[i] = pos[i] | neg[i];
+  }
+  for (int p = 0; p < npeel; ++p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t lz;  // v_ffbh_u32: leading zeros, 0xffffffff for 0 (defined, unlike clz(0))
+      asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(rest[i]));
+      rest[i] &= ~(0x80000000u >> (lz & 31));
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t keep = (pos[i] | neg[i]) ^ rest[i];
+    v[i] = (int32_t)(pos[i] & keep) - (int32_t)(neg[i] & keep);
+  }
+}
+
+// Peel count of the fast path for code maxv = 2^bw - 1 and k kept terms.
+__device__ __forceinline__ int relu_peels(float maxv, int k) {
+  const int bw = 32 - __builtin_clz((uint32_t)maxv | 1u);
+  return k < hese_max_terms(bw) ? k : hese_max_terms(bw);
+}
+
 // Activation / weight code formats of the term-pair kernels (include/tq.h TQ_CODES_*):
 // the same signed integer term sum v stored as int16 (VALU dot2 engine) or as the fp16
 // value v (MFMA engine; exact for |v| <= 2048, i.e. bitwidth <= 11).
@@ -113,7 +159,9 @@ constexpr int kCodesI16 = 0;
 constexpr int kCodesF16 = 1;
 
 __device__ __forceinline__ uint32_t code_bits(int32_t v, int fmt) {
-  return fmt == kCodesF16 ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v)
+  // |v| <= 2^bitwidth <= 2^14 (max_code_bits), so the int16 -> fp16 conversion
+  // (v_cvt_f16_i16, one rounding) equals the int32 -> fp16 one
+  return fmt == kCodesF16 ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(int16_t)v)
                           : ((uint32_t)v & 0xFFFFu);
 }
 

@@ -32,10 +32,17 @@ __device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4
 
 __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, int co,
                                              const float y[4], double inv_sf, float maxv,
-                                             int k, int fmt) {
+                                             int k, int fmt, bool relu) {
   uint32_t v[4];
+  if (relu && inv_sf <= 1.0e308) {  // y >= 0 and sf > 0: the sign-free fast path
+    int32_t t[4];
+    tr_values_relu4(y, inv_sf, maxv, relu_peels(maxv, k), t);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = code_bits(tr_value_g1_inv(y[i], inv_sf, maxv, k), fmt);
+    for (int i = 0; i < 4; ++i) v[i] = code_bits(t[i], fmt);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = code_bits(tr_value_g1_inv(y[i], inv_sf, maxv, k), fmt);
+  }
   *reinterpret_cast<int2*>(codes + p * cp + co) =
       make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
 }
@@ -61,8 +68,10 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
   }
   if (a.out)
     *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(y[0], y[1], y[2], y[3]);
-  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a);
-  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b);
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
+                               a.relu);
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
+                               a.relu);
 }
 
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
@@ -102,8 +111,10 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
         if (co + i < a.Cout) dst[i] = y[i];
     }
   }
-  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a);
-  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b);
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
+                               a.relu);
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
+                               a.relu);
 }
 
 // Bijective XCD-aware remap of the block index: blocks are dealt round-robin to the 8 XCDs

@@ -328,3 +328,52 @@ def test_stem_weight_split_is_exact():
         assert abs(float(tot[o, idx]) - float(w[o, c, r, q])) <= 2.0**-26 * abs(float(w[o, c, r, q]))
     with pytest.raises(RuntimeError):
         tq_ops.pack_stem_weight(torch.zeros(64, 3, 5, 5))
+
+
+def _hese_masks_np(q):
+    hi, lo = q >> 1, q << 1
+    a = q & ~hi
+    return (a & ~lo) | ((a & lo) << 1), q & hi & ~lo
+
+
+def _popcount_np(m):
+    c = np.zeros_like(m)
+    while m.any():
+        c += m & 1
+        m = m >> 1
+    return c
+
+
+def test_hese_max_terms():
+    """csrc/tq_device.h hese_max_terms: the largest HESE term count of a bw-bit magnitude is
+    floor(2 (bw + 1) / 3) (the epilogue fast path caps its top-bit peels there)."""
+    for bw in range(1, 21):
+        pos, neg = _hese_masks_np(np.arange(1 << bw, dtype=np.int64))
+        assert _popcount_np(pos | neg).max() == 2 * (bw + 1) // 3, bw
+
+
+def test_relu_fast_path_restatement():
+    """csrc/tq_device.h tr_values_relu4, restated in numpy: the fract-based rounding and the
+    top-bit peel (capped at hese_max_terms) give the oracle's TR value for y >= 0."""
+    rng = np.random.default_rng(0)
+    for bw, k in [(9, 3), (9, 0), (9, 1), (9, 12), (8, 8), (11, 4), (4, 2), (14, 5)]:
+        maxv = np.float32(2 ** bw - 1)
+        sf = np.float32(0.037)
+        y = np.concatenate([rng.exponential(2.0 ** bw * 0.02, 20000),
+                            (np.arange(0, 2 ** bw + 8) + 0.5) * 0.037,
+                            [0.0, np.inf, 1e30]]).astype(np.float32)
+        r = np.minimum((y.astype(np.float64) * (1.0 / np.float64(sf))).astype(np.float32), maxv)
+        fl = np.floor(r)
+        q = (fl.astype(np.int64) + ((r - fl) >= 0.5)).astype(np.int64)
+        pos, neg = _hese_masks_np(q)
+        m = pos | neg
+        rest = m.copy()
+        for _ in range(min(k, 2 * (bw + 1) // 3)):
+            nz = rest > 0
+            top = np.zeros_like(rest)
+            top[nz] = 1 << np.floor(np.log2(rest[nz])).astype(np.int64)
+            rest = rest & ~top
+        keep = m ^ rest
+        got = (pos & keep) - (neg & keep)
+        exp = oracle.tr(y.reshape(1, -1, 1, 1), float(sf), bw, 1, k).reshape(-1) / sf
+        np.testing.assert_array_equal(got.astype(np.float64), np.round(exp.astype(np.float64)))
