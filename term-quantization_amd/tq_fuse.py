@@ -97,6 +97,15 @@ class _Conv(object):
         return out, ca, cb
 
 
+def _same_codes(a, b):
+    """True when two consumers of one activation would get identical codes: same TR
+    parameters (sf, data bits, data terms), code format and channel padding.  A block's conv1
+    and downsample read the same tensor, so their calibrated quantizers agree and the
+    downsample reuses conv1's codes instead of a second encode + store."""
+    return ([float(v) for v in a.quant] == [float(v) for v in b.quant] and
+            a.code_dtype == b.code_dtype and a.cp_in == b.cp_in)
+
+
 class _Block(object):
     def __init__(self, block):
         self.conv1 = _Conv(block.conv1, block.bn1)
@@ -150,7 +159,8 @@ class FusedResNet(nn.Module):
         codes = torch.empty((n, h // 4, w // 4, first.conv1.cp_in),
                             dtype=first.conv1.code_dtype, device=x.device)
         codes_down = None
-        if first.down is not None:
+        shared = first.down is not None and _same_codes(first.conv1, first.down)
+        if first.down is not None and not shared:
             codes_down = torch.empty((n, h // 4, w // 4, first.down.cp_in),
                                      dtype=first.down.code_dtype, device=x.device)
         # work = the stem conv's fp32 MACs (7x7x3 per output of the 64 x H/2 x W/2 conv)
@@ -159,8 +169,8 @@ class FusedResNet(nn.Module):
             lambda: tq_native.stem_conv_pool_encode(
                 x, self.stem_w, self.stem_scale, self.stem_shift, out, codes_a=codes,
                 quant_a=first.conv1.quant, codes_b=codes_down,
-                quant_b=first.down.quant if first.down is not None else None))
-        return out, codes, codes_down
+                quant_b=first.down.quant if codes_down is not None else None))
+        return out, codes, (codes if shared else codes_down)
 
     def _stem(self, x):
         m = self.qmodel
@@ -214,10 +224,13 @@ class FusedResNet(nn.Module):
                 identity, _, _ = b.down(codes_down, out=True)
             else:
                 identity = x
+            next_b = nxt.down if nxt is not None and nxt.down is not None else None
+            shared = next_b is not None and _same_codes(nxt.conv1, next_b)
             x, codes, codes_down = b.conv2(
                 mid, out=True, residual=identity, relu=True,
-                next_a=nxt.conv1 if nxt else None,
-                next_b=nxt.down if nxt is not None and nxt.down is not None else None)
+                next_a=nxt.conv1 if nxt else None, next_b=None if shared else next_b)
+            if shared:
+                codes_down = codes
         x = m.avgpool(x)
         x = torch.flatten(x, 1)
         return m.fc(x)

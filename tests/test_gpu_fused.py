@@ -104,6 +104,27 @@ def test_fused_resnet_matches_module_path(engine, fused_stem):
     assert (got.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.75
 
 
+def test_fused_resnet_shared_downsample_codes(monkeypatch):
+    """A block's conv1 and downsample read one tensor, so their calibrated quantizers agree
+    and the executor encodes it once; the result is bit-identical to encoding it twice."""
+    torch.manual_seed(0)
+    model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        q(x)
+    tr_layer.set_tr_tracking(q, False)
+    fused = tq_fuse.FusedResNet(q)
+    downs = [b for b in fused.blocks if b.down is not None]
+    assert downs and all(tq_fuse._same_codes(b.conv1, b.down) for b in downs)
+    with torch.no_grad():
+        shared = fused(x)
+        monkeypatch.setattr(tq_fuse, "_same_codes", lambda a, b: False)
+        separate = fused(x)
+    assert torch.equal(shared, separate)
+
+
 @pytest.mark.parametrize("layer,cfgs", [(1, [(2, 1), (2, -1), (6, -1)]),
                                          (6, [(1, 1), (1, -1), (5, -1), (4, -1)]),
                                          (16, [(1, 1), (1, -1), (4, -1), (4, 3)]),
