@@ -299,14 +299,14 @@ def main():
             "share_of_step": conv["seconds"] / elapsed,
         })
         if enc_name == "stem_conv_pool":
-            # the fused stem: fp32-class conv on split-bf16 MFMAs + BN/ReLU/pool + codes;
+            # the fused stem: near-fp32 conv on split-fp16 MFMAs + BN/ReLU/pool + codes;
             # algorithmic work = the reference's fp32 conv MACs, priced against the fp32
             # peak (the arithmetic the reference runs, 157.3 TFLOP/s MFMA/VALU)
             n_img = args.batch
             stem_bytes = n_img * (3 * 224 * 224 * 4 + 64 * 56 * 56 * (4 + 2))
             roof_tr = {
-                "kernel": "stem_conv_pool_kernel (ResNet stem conv 7x7/2 in fp32 arithmetic on "
-                          "split-bf16 v_mfma_f32_16x16x32_bf16 + BN/ReLU/max-pool + first "
+                "kernel": "stem_conv_pool_kernel (ResNet stem conv 7x7/2 in near-fp32 arithmetic "
+                          "on split-fp16 v_mfma_f32_16x16x32_f16 + BN/ReLU/max-pool + first "
                           "activation TR -> fp16 codes)",
                 "bound": "mfma",
                 "achieved": 2 * enc_bytes / enc_t / 1e12,

@@ -229,14 +229,16 @@ int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, i
 /*
  * The whole stem of a TQ ResNet in one pass (torchvision ResNet.forward: conv1 -> bn1 -> relu
  * -> maxpool, then the first TR layers' input TR, tr_layer.py:96-99): conv 7x7 stride 2
- * pad 3, 3 -> 64 channels, no bias, in fp32 arithmetic on the bf16 matrix cores (three-way
- * bf16 split of inputs and weights, six partial products per pair; per-product relative
- * error ~2^-25, the class of the reference's fp32 cuDNN conv), eval BatchNorm
+ * pad 3, 3 -> 64 channels, no bias, in near-fp32 arithmetic on the fp16 matrix cores
+ * (two-way fp16 split of inputs, scaled per tile by a power of two, and of the weights,
+ * three partial products per pair, fp32 accumulation; per-product relative error ~2^-21,
+ * between the reference's fp32 cuDNN conv and cuDNN's default TF32), eval BatchNorm
  * out = conv * scale[c] + shift[c] (fp32 fma), ReLU, max-pool 3x3 stride 2 pad 1, fp32
  * output and codes as tq_bn_relu_maxpool_encode.  The 64 x (H/2) x (W/2) conv output never
  * goes to memory.
  *   x        fp32 channels_last image [n][h][w][3], 8-byte aligned; h, w multiples of 4
- *   w_split  [3][64][192] bf16 bits: the three splits of the conv weight in space-to-depth
+ *   w_split  [2][64][192] fp16 bits: the two splits of the conv weight * 2^10 (|w| <= 32) in
+ *            space-to-depth
  *            K order k = ((sy*4 + sx)*2 + sub_r)*6 + sub_c*3 + c for tap (2sy+sub_r-1,
  *            2sx+sub_c-1), zero where a tap index is -1 (term-quantization_amd/tq_ops.py
  *            pack_stem_weight)

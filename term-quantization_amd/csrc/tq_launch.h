@@ -82,7 +82,7 @@ struct PoolArgs {
   int fmt_a, fmt_b;
   double inv_a, inv_b;   // RN64(1 / sf_a), RN64(1 / sf_b)
   // fused stem (tq_stem_conv.hip): x is the [N][H][W][3] input image, H/W its size, and
-  // wsplit the conv weights as three bf16 splits [3][64][192] (s2d K order)
+  // wsplit the conv weights * 2^10 as two fp16 splits [2][64][192] (s2d K order)
   const uint16_t* wsplit;
 };
 

@@ -7,25 +7,30 @@
 // writing a 256x64x112x112 tensor (822 MB), a pass reading it back, and the pool output; here
 // the conv output never leaves the chip: HBM sees the 154 MB input and the pooled outputs.
 //
-// fp32 arithmetic on bf16 matrix cores (split-bf16, "bf16x3").  Every fp32 value is split
-// exactly-rounded into three bf16 parts, x = x0 + x1 + x2 + e with |x1| <= 2^-9 |x|,
-// |x2| <= 2^-18 |x|, |e| <= 2^-27 |x| (each part is RN(bf16) of the exact remainder; the
-// remainders are exact fp32 differences, Sterbenz).  Weights are split the same way on the
-// host.  The products x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0 (6 MFMAs) are exact in fp32 and
-// are accumulated in fp32 by the MFMA; the dropped terms are below 2^-26 |x||w|, so each
-// product carries ~2^-25 relative error -- the accuracy class of an fp32 conv, whose own
-// summation order (cuDNN / MIOpen algorithm choice) the reference does not fix either.
+// Near-fp32 arithmetic on fp16 matrix cores ("fp16x2").  Every fp32 value is split exactly
+// into two fp16 parts, v = v0 + v1 + e with v0 = RN16(v), v1 = RN16(v - v0) (the remainder is
+// exact in fp32), |e| <= 2^-22 |v| while v1 is a normal fp16.  fp16 needs a range: the host
+// packs the weights as w * 2^10 (|w| <= 32), and each tile's inputs are scaled in LDS by a
+// power of two 2^kx chosen from the tile's max |x| (reduced while staging) so that it lies
+// in [2^13, 2^14); the sums are scaled back by 2^-(kx + 10) (exact) before BN.  The products
+// x0w0 + x0w1 + x1w0 (3 MFMAs) are exact in fp32 and accumulate in fp32; dropped terms and
+// split errors are below ~3 * 2^-22 |x||w| (~7e-7: an fp32 conv's accumulation-order
+// differences are ~1e-7, a TF32 conv -- cuDNN's default for convs on Ampere -- ~5e-4).  Input
+// values below 2^-17 of their tile's max lose relative precision (fp16 subnormal remainder,
+// absolute error <= 2^-25 in scaled units); the test bound 1e-5 * sum |x||w| holds unless a
+// whole 7x7 window sits below ~2^-22 of its tile's max.  An earlier split-bf16 version
+// (three parts, 6 MFMAs, 2^-25) measured 610 us for the bench batch.
 //
 // Layout.  Space-to-depth turns the stride-2 7x7 conv into a stride-1 4x4 conv over 12
 // channels: the kernel padded to 8x8 (a zero tap in front), s2d pixel (R, C) = input rows
 // 2R, 2R+1 x cols 2C, 2C+1 x 3 channels = 12 values; conv pixel (oy, ox) reads s2d rows
 // oy-2..oy+1 and cols ox-2..ox+1, so K = 4 x 4 x 12 = 192 in the order (sy, sx, sub_r, sub_c,
 // c), and any 8 consecutive K values are 8 consecutive fp32 in an s2d row ([col][12] rows).
-//   LDS: weights [3 splits][64 rows of 208 bf16] (80 KB, staged once per workgroup) and
+//   LDS: weights [2 splits][64 rows of 208 fp16] (53 KB, staged once per workgroup) and
 //        the input tile as fp32 s2d rows [2TP+4][SC][12] (46 KB for TP = 2, W = 224)
 //   wave = one strip of 16 conv columns (7 pool columns) x 2TP+1 conv rows, two rows at a
-//        time; per row 6 K-steps x (4 Cout blocks x 6 split products)
-//        v_mfma_f32_16x16x32_bf16, each weight fragment read once for both rows
+//        time; per row 6 K-steps x (4 Cout blocks x 3 split products)
+//        v_mfma_f32_16x16x32_f16, each weight fragment read once for both rows
 //   epilogue: BN (fp32 fma, as the stem-tail kernel) + ReLU, vertical max over the 3 conv
 //        rows of each pool row in registers, horizontal max by lane shuffles (width 16), the
 //        strip's 7 pool pixels x 64 channels compacted through LDS (1.8 KB per wave), then
@@ -41,26 +46,26 @@ namespace tq {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kStemThreads = 512;
 constexpr int kStemK = 192;     // s2d K
 constexpr int kStemWRow = 208;  // LDS weight row (bf16): 416 B makes the A reads conflict-free
-constexpr int kStemWBytes = 3 * 64 * kStemWRow * 2;
+constexpr int kStemWBytes = 2 * 64 * kStemWRow * 2;
+constexpr int kStemWExp = 10;   // weights are split as w * 2^10 (tq_ops.pack_stem_weight)
+constexpr int kStemXMag = 14;   // a tile's inputs are scaled to max |x| < 2^14
+constexpr int kStemDynLds = 160 * 1024 - 256;  // the rest of the CU's LDS: static tile_max
 
-__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& x0, bf16x8& x1,
-                                       bf16x8& x2) {
+// x = x0 + x1 + e: x0 = RN16(x), x1 = RN16(x - x0) (the remainder is exact in fp32: a
+// multiple of ulp32(x) below ulp16(x)); |e| <= 2^-22 |x| while x1 is a normal fp16.
+__device__ __forceinline__ void split2(const float (&x)[8], f16x8& x0, f16x8& x1) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const __bf16 h0 = (__bf16)x[j];
-    const float r1 = x[j] - (float)h0;
-    const __bf16 h1 = (__bf16)r1;
-    const float r2 = r1 - (float)h1;
+    const _Float16 h0 = (_Float16)x[j];
     x0[j] = h0;
-    x1[j] = h1;
-    x2[j] = (__bf16)r2;
+    x1[j] = (_Float16)(x[j] - (float)h0);
   }
 }
 
@@ -68,6 +73,7 @@ template <int TP>
 __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArgs a, int sc,
                                                                          int nb, int tiles) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds_raw[];
+  __shared__ uint32_t tile_max[2];  // max |x| (fp32 bits) of a tile's rows, by tile parity
   uint16_t* ws = reinterpret_cast<uint16_t*>(lds_raw);
   float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(lds_raw) + kStemWBytes);
   // per-wave pool staging: 7 pixels x 64 channels fp32 behind the input rows
@@ -80,8 +86,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   const int Hc = a.H / 2, Wc = a.W / 2;  // conv output
   const int tpi = (a.Ho + TP - 1) / TP;  // tiles per image
 
-  // weights once per workgroup: [3][64][192] bf16 -> rows of kStemWRow
-  for (int i = tid; i < 3 * 64 * (kStemK / 8); i += kStemThreads) {
+  // weights once per workgroup: [2][64][192] fp16 -> rows of kStemWRow
+  for (int i = tid; i < 2 * 64 * (kStemK / 8); i += kStemThreads) {
     const int row = i / (kStemK / 8);
     const int ch = i - row * (kStemK / 8);
     *reinterpret_cast<u32x4*>(ws + row * kStemWRow + ch * 8) =
@@ -125,7 +131,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       }
     }
   };
-  auto commit = [&]() {
+  auto commit = [&](int kx) {  // rows scaled by 2^kx (exact while no underflow)
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const int rid = wave + 8 * r;
@@ -138,20 +144,55 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         // flat input-row float f -> s2d column 3 + f / 6, slot f % 6 of the sub row
         const int f = 4 * idx;
         *reinterpret_cast<float2*>(row + (3 + f / 6) * 12 + f % 6) =
-            make_float2(pre[r][q].x, pre[r][q].y);
+            make_float2(ldexpf(pre[r][q].x, kx), ldexpf(pre[r][q].y, kx));
         *reinterpret_cast<float2*>(row + (3 + (f + 2) / 6) * 12 + (f + 2) % 6) =
-            make_float2(pre[r][q].z, pre[r][q].w);
+            make_float2(ldexpf(pre[r][q].z, kx), ldexpf(pre[r][q].w, kx));
       }
     }
   };
+  if (tid == 0) {
+    tile_max[0] = 0u;
+    tile_max[1] = 0u;
+  }
   if (blockIdx.x < tiles) prefetch(blockIdx.x);
+  __syncthreads();
 
-  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+  // fp16 operands need a range: each tile's inputs are scaled by 2^kx so that max |x| <
+  // 2^14 (a power of two: exact), and the conv sums are scaled back by 2^-(kx + kStemWExp)
+  // before BN.  The tile max is reduced while the rows are still in registers; slot
+  // (it & 1) is written before barrier A and read between A and B, the other slot is
+  // cleared between A and B for the next tile.
+  int it = 0;
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, ++it) {
     const int n = tile / tpi;
     const int py0 = (tile - n * tpi) * TP;
-    __syncthreads();  // the previous tile's s2d rows are no longer read (and xs is zeroed)
-    commit();
-    __syncthreads();
+    {
+      uint32_t lm = 0u;
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int q = 0; q < QMAX; ++q) {
+          lm = max(lm, __float_as_uint(pre[r][q].x) & 0x7fffffffu);
+          lm = max(lm, __float_as_uint(pre[r][q].y) & 0x7fffffffu);
+          lm = max(lm, __float_as_uint(pre[r][q].z) & 0x7fffffffu);
+          lm = max(lm, __float_as_uint(pre[r][q].w) & 0x7fffffffu);
+        }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) lm = max(lm, (uint32_t)__shfl_xor((int)lm, off));
+      if (lane == 0) atomicMax(&tile_max[it & 1], lm);
+    }
+    __syncthreads();  // A: the previous tile's s2d rows are no longer read, tile max is final
+    const uint32_t mbits = tile_max[it & 1];
+    int kx = 0;  // all-zero or non-finite tiles stay unscaled
+    if (mbits != 0u && mbits < 0x7f800000u) {
+      int e;
+      frexpf(__uint_as_float(mbits), &e);  // max |x| in [2^(e-1), 2^e)
+      kx = kStemXMag - e;
+    }
+    const int kback = -(kx + kStemWExp);
+    commit(kx);
+    if (tid == 0) tile_max[(it + 1) & 1] = 0u;
+    __syncthreads();  // B
     if (tile + (int)gridDim.x < tiles) prefetch(tile + gridDim.x);
 
     for (int b = wave; b < nb; b += kStemThreads / 64) {
@@ -188,25 +229,21 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll
             for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 1, xn[r]);
           }
-          bf16x8 x0[NR], x1[NR], x2[NR];
+          f16x8 x0[NR], x1[NR];
 #pragma unroll
-          for (int r = 0; r < NR; ++r) split3(xc[r], x0[r], x1[r], x2[r]);
+          for (int r = 0; r < NR; ++r) split2(xc[r], x0[r], x1[r]);
           {
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) {
             const uint16_t* wr = ws + (mb * 16 + i16) * kStemWRow + 32 * ks + 8 * g;
-            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(wr);
-            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(wr + 64 * kStemWRow);
-            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(wr + 128 * kStemWRow);
+            const f16x8 w0 = *reinterpret_cast<const f16x8*>(wr);
+            const f16x8 w1 = *reinterpret_cast<const f16x8*>(wr + 64 * kStemWRow);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
               f32x4 c = acc[r][mb];
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x0[r], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x1[r], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x0[r], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, x2[r], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1[r], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x0[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, x0[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, x1[r], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, x0[r], c, 0, 0, 0);
               acc[r][mb] = c;
             }
           }
@@ -224,7 +261,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float v = fmaf(acc[r][mb][i], bsc[mb][i], bsh[mb][i]);
+              const float v = fmaf(ldexpf(acc[r][mb][i], kback), bsc[mb][i], bsh[mb][i]);
               y[r][mb][i] = ok ? fmaxf(v, 0.0f) : 0.0f;
             }
         }
@@ -310,11 +347,11 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
   const int64_t bytes =
       kStemWBytes + (int64_t)(2 * TP + 4) * sc * 12 * 4 + (kStemThreads / 64) * 7 * 64 * 4;
-  if (bytes > 160 * 1024) return hipErrorInvalidConfiguration;
+  if (bytes > kStemDynLds) return hipErrorInvalidConfiguration;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kStemDynLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }

@@ -150,7 +150,10 @@ class FusedResNet(nn.Module):
                 and c1.kernel_size == (7, 7) and c1.stride == (2, 2) and c1.padding == (3, 3)
                 and c1.dilation == (1, 1) and c1.groups == 1 and c1.bias is None
                 and c1.weight.dtype == torch.float32):
-            self.stem_w = tq_ops.pack_stem_weight(c1.weight)
+            try:
+                self.stem_w = tq_ops.pack_stem_weight(c1.weight)
+            except RuntimeError:  # weights outside the fp16 split's range: unfused stem
+                self.stem_w = None
 
     def _stem_fused(self, x, first):
         n, _, h, w = x.shape

@@ -179,23 +179,30 @@ def mfma_flush_steps(packed, data_bits):
     return 0 if best == s else best
 
 
+STEM_W_EXP = 10      # csrc/tq_stem_conv.hip kStemWExp: weights are packed as w * 2^10
+STEM_W_MAX = 32.0    # |w| * 2^10 stays below the fp16 range (65504)
+
+
 def pack_stem_weight(w):
-    """ResNet stem conv weight [64, 3, 7, 7] fp32 -> [3, 64, 192] bf16 bits (int16 tensor) for
+    """ResNet stem conv weight [64, 3, 7, 7] fp32 -> [2, 64, 192] fp16 bits (int16 tensor) for
     tq_stem_conv_pool_encode: the 7x7 kernel padded to 8x8 with a leading zero tap, in
-    space-to-depth K order (sy, sx, sub_r, sub_c, c), split exactly into three bf16 parts
-    w = w0 + w1 + w2 + e (each RN(bf16) of the remainder, |e| <= 2^-27 |w|)."""
+    space-to-depth K order (sy, sx, sub_r, sub_c, c), scaled by 2^10 (exact) and split into
+    two fp16 parts w * 2^10 = w0 + w1 + e (w0 = RN16, w1 = RN16 of the exact remainder,
+    |e| <= 2^-22 |w| * 2^10 while w1 is normal).  Raises RuntimeError for weights the fp16
+    range cannot hold (|w| > 32 or non-finite); the executor then keeps the unfused stem."""
     if tuple(w.shape) != (64, 3, 7, 7) or w.dtype != torch.float32:
         raise RuntimeError("pack_stem_weight: expects a [64, 3, 7, 7] float32 weight")
+    wd = w.detach()
+    if not bool(torch.isfinite(wd).all()) or float(wd.abs().max()) > STEM_W_MAX:
+        raise RuntimeError("pack_stem_weight: weights must be finite with |w| <= %g"
+                           % STEM_W_MAX)
     w8 = torch.zeros((64, 3, 8, 8), dtype=torch.float32, device=w.device)
-    w8[:, :, 1:, 1:] = w.detach()
+    w8[:, :, 1:, 1:] = wd * (2.0 ** STEM_W_EXP)
     # [o, c, sy, sub_r, sx, sub_c] -> [o, sy, sx, sub_r, sub_c, c]
     k = w8.view(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(64, 192)
-    w0 = k.to(torch.bfloat16)
-    r1 = k - w0.float()
-    w1 = r1.to(torch.bfloat16)
-    r2 = r1 - w1.float()
-    w2 = r2.to(torch.bfloat16)
-    return torch.stack([w0, w1, w2]).contiguous().view(torch.int16)
+    w0 = k.to(torch.float16)
+    w1 = (k - w0.float()).to(torch.float16)
+    return torch.stack([w0, w1]).contiguous().view(torch.int16)
 
 
 def mfma_flush_chunk(packed, data_bits, cp, ntaps):

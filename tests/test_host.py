@@ -310,24 +310,36 @@ def test_mfma_flush_chunk_windows_cover_chunk_major_order():
 
 
 def test_stem_weight_split_is_exact():
-    """pack_stem_weight: three bf16 parts summing to the fp32 weight within 2^-26 relative, in
-    the space-to-depth K order of the stem kernel (zero taps where the 8x8 pad is)."""
+    """pack_stem_weight: two fp16 parts of w * 2^10 summing to the fp32 weight within 2^-22
+    relative (2^-35 absolute once the remainder is an fp16 subnormal), in the space-to-depth
+    K order of the stem kernel (zero taps where the 8x8 pad is); out-of-range weights are
+    refused."""
     import tq_ops  # noqa: F811
     torch.manual_seed(4)
     w = torch.randn(64, 3, 7, 7) * 0.07
-    parts = tq_ops.pack_stem_weight(w).view(torch.bfloat16).double()  # [3, 64, 192]
-    tot = parts.sum(0)
+    w[0, 0, 0, 0] = 31.9
+    w[1, 1, 1, 1] = 3e-7
+    parts = tq_ops.pack_stem_weight(w).view(torch.float16).double()  # [2, 64, 192]
+    assert tuple(parts.shape) == (2, 64, 192)
+    tot = parts.sum(0) * 2.0**-tq_ops.STEM_W_EXP
     w8 = torch.zeros(64, 3, 8, 8, dtype=torch.float64)
     w8[:, :, 1:, 1:] = w.double()
     k = w8.view(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(64, 192)
-    assert bool(((tot - k).abs() <= 2.0**-26 * k.abs()).all())
+    bound = 2.0**-22 * k.abs() + 2.0**-35
+    assert bool(((tot - k).abs() <= bound).all())
     # K index k = ((sy*4 + sx)*2 + sub_r)*6 + sub_c*3 + c  <->  tap (2sy+sub_r-1, 2sx+sub_c-1)
     for (o, c, r, q) in [(0, 0, 0, 0), (5, 2, 6, 6), (63, 1, 3, 4)]:
         kh8, kw8 = r + 1, q + 1
         idx = ((kh8 // 2 * 4 + kw8 // 2) * 2 + kh8 % 2) * 6 + (kw8 % 2) * 3 + c
-        assert abs(float(tot[o, idx]) - float(w[o, c, r, q])) <= 2.0**-26 * abs(float(w[o, c, r, q]))
+        wv = float(w[o, c, r, q])
+        assert abs(float(tot[o, idx]) - wv) <= 2.0**-22 * abs(wv) + 2.0**-35
     with pytest.raises(RuntimeError):
         tq_ops.pack_stem_weight(torch.zeros(64, 3, 5, 5))
+    for bad in (33.0, float("inf"), float("nan")):
+        wb = w.clone()
+        wb[3, 2, 1, 0] = bad
+        with pytest.raises(RuntimeError, match="finite"):
+            tq_ops.pack_stem_weight(wb)
 
 
 def _hese_masks_np(q):
