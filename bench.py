@@ -314,6 +314,9 @@ def main():
                 "unit": "TFLOP/s (fp32-equivalent)",
                 "frac": 2 * enc_bytes / enc_t / 1e12 / FP32_PEAK_TFLOPS,
                 "hbm_gbs": stem_bytes / enc_t / 1e9,
+                # what the matrix cores execute: 3 fp16 split products per fp32 MAC
+                "mfma_f16_tflops": 3 * 2 * enc_bytes / enc_t / 1e12,
+                "mfma_f16_frac": 3 * 2 * enc_bytes / enc_t / 1e12 / MFMA_F16_PEAK_TFLOPS,
                 "traffic": enc_traffic,
                 "algorithmic_macs_per_launch": enc_bytes,
                 "avg_launch_us": enc_t * 1e6,
