@@ -69,6 +69,14 @@ __device__ __forceinline__ void split2(const float (&x)[8], f16x8& x0, f16x8& x1
   }
 }
 
+// __shfl_down(v, D, 16) as a DPP row shift (no LDS permute): lane i of each 16-lane row
+// reads lane i + D; lanes whose source is past the row end keep their own value.
+template <int D>
+__device__ __forceinline__ float row_down(float v) {
+  const int b = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(b, b, 0x100 + D, 0xf, 0xf, false));
+}
+
 template <int TP>
 __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArgs a, int sc,
                                                                          int nb, int tiles) {
@@ -277,8 +285,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float v = fmaxf(run[mb][i], last[mb][i]);
-            const float v1 = __shfl_down(v, 1, 16);
-            const float v2 = __shfl_down(v, 2, 16);
+            const float v1 = row_down<1>(v);
+            const float v2 = row_down<2>(v);
             m[mb][i] = fmaxf(fmaxf(v, v1), v2);
           }
         // compact the strip's 7 pool pixels x 64 channels through LDS, then every lane
@@ -316,9 +324,16 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             const int cp = side ? a.cp_b : a.cp_a;
             const int fmt = side ? a.fmt_b : a.fmt_a;
             uint32_t v[4];
+            if (inv <= 1.0e308) {  // yv >= 0 (ReLU, then max): the sign-free fast path
+              int32_t t[4];
+              tr_values_relu4(yv, inv, maxv, relu_peels(maxv, k), t);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              v[i] = code_bits(tr_value_g1_inv(yv[i], inv, maxv, k), fmt);
+              for (int i = 0; i < 4; ++i) v[i] = code_bits(t[i], fmt);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                v[i] = code_bits(tr_value_g1_inv(yv[i], inv, maxv, k), fmt);
+            }
             *reinterpret_cast<int2*>(codes + p * cp + co) =
                 make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
           }
