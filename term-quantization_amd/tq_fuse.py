@@ -229,8 +229,10 @@ class FusedResNet(nn.Module):
                 identity = x
             next_b = nxt.down if nxt is not None and nxt.down is not None else None
             shared = next_b is not None and _same_codes(nxt.conv1, next_b)
+            # a block followed by a downsampling block: its fp32 output is nobody's residual
+            # (the next identity is the downsample conv's), so only its codes are written
             x, codes, codes_down = b.conv2(
-                mid, out=True, residual=identity, relu=True,
+                mid, out=True if next_b is None else None, residual=identity, relu=True,
                 next_a=nxt.conv1 if nxt else None, next_b=None if shared else next_b)
             if shared:
                 codes_down = codes
