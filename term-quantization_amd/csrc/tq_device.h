@@ -113,7 +113,7 @@ __device__ __forceinline__ int32_t tr_value_g1_inv(float x, double inv_sf, float
 }
 
 // Epilogue fast path for 4 values the epilogue has just passed through ReLU (y >= 0, never
-// NaN) with a finite inv_sf (sf > 0): no sign, no NaN test, and the a1 rounding as
+// NaN) with 0 < sf < inf (finite, nonzero inv_sf): no sign, no NaN test, and the a1 rounding as
 //   q = cvt(min(r, maxv)) + (fract(min(r, maxv)) >= 0.5)
 // (exact: floor(r + 0.5) = floor(r) + (r - floor(r) >= 0.5); the clamp keeps +inf out of
 // fract, and at the clamp fract(maxv) = 0 since maxv is an integer).  Top-k selection

@@ -34,7 +34,7 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, 
                                              const float y[4], double inv_sf, float maxv,
                                              int k, int fmt, bool relu) {
   uint32_t v[4];
-  if (relu && inv_sf <= 1.0e308) {  // y >= 0 and sf > 0: the sign-free fast path
+  if (relu && inv_sf > 0.0 && inv_sf <= 1.0e308) {  // y >= 0, 0 < sf < inf: fast path
     int32_t t[4];
     tr_values_relu4(y, inv_sf, maxv, relu_peels(maxv, k), t);
 #pragma unroll

@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             const int cp = side ? a.cp_b : a.cp_a;
             const int fmt = side ? a.fmt_b : a.fmt_a;
             uint32_t v[4];
-            if (inv <= 1.0e308) {  // yv >= 0 (ReLU, then max): the sign-free fast path
+            if (inv > 0.0 && inv <= 1.0e308) {  // yv >= 0 (ReLU, max), 0 < sf < inf: fast path
               int32_t t[4];
               tr_values_relu4(yv, inv, maxv, relu_peels(maxv, k), t);
 #pragma unroll

@@ -104,6 +104,35 @@ def test_fused_resnet_matches_module_path(engine, fused_stem):
     assert (got.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.75
 
 
+@pytest.mark.parametrize("sf", [0.0, float("inf"), 1e-38, 1e30])
+def test_fused_epilogue_codes_extreme_scales(sf, engine):
+    """Next-layer codes at scales outside the fast path's range or at its edges: sf = 0
+    (|y|/0 -> maxv, 0/0 -> 0), sf = inf (-> 0), tiny sf (saturates), huge sf (rounds to 0
+    or 1 term).  Expected values follow kernels/tr_cuda_kernel.cu:21-23 directly."""
+    layer, bn = _layer(64, 64, 3, 1, seed=5)
+    conv = tq_fuse._Conv(layer, bn)
+    nxt, _ = _layer(64, 64, 3, 1, seed=99)
+    nxt.input_quant.sf = sf
+    nxt_conv = tq_fuse._Conv(nxt, None)
+    torch.manual_seed(8)
+    x = torch.relu(torch.randn(2, 64, 9, 9, device=DEV))
+    codes = torch.empty((2, 9, 9, conv.cp_in), dtype=conv.code_dtype, device=DEV)
+    tq_native.act_encode(x.contiguous(memory_format=torch.channels_last), True, 0.03, 9, 3,
+                         codes)
+    y, ca, _ = conv(codes, out=True, relu=True, next_a=nxt_conv)
+    yn = y.contiguous().cpu().numpy()
+    got = ca.cpu().long()[..., :64].permute(0, 3, 1, 2).numpy()
+    if sf == float("inf"):
+        exp = np.zeros_like(got)
+    elif sf == 0.0 or sf == 1e-38:
+        exp = np.where(yn > 0, 511, 0)  # TR of maxv = 511 = 512 - 1: two terms, value 511
+    else:
+        exp = np.rint(oracle.tr(yn.reshape(1, -1, 1, 1), sf, 9, 1, 3).reshape(yn.shape) /
+                      np.float32(sf)).astype(np.int64)
+    assert (yn > 0).any()
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_fused_resnet_shared_downsample_codes(monkeypatch):
     """A block's conv1 and downsample read one tensor, so their calibrated quantizers agree
     and the executor encodes it once; the result is bit-identical to encoding it twice."""
