@@ -134,13 +134,18 @@ def sweep(args, dev):
         sc = torch.full((cout,), 1e-4, dtype=torch.float64, device=dev)
         sh = torch.zeros(cout, dtype=torch.float64, device=dev)
         mac = args.batch * cout * ho * ho * cin * k * k
+        # the bench's heavier epilogue: ReLU, fp32 output and next-layer codes
+        ca = torch.empty((args.batch, ho, ho, tq_ops.act_channels(cout)),
+                         dtype=layer.w_codes.dtype, device=dev)
         res = {}
         for cfg in range(0, ncfg + 1):
             for sp in ([1, -1, 3] if cfg and not mfma else [0]):
                 fn = lambda: tq_native.conv2d_termpair_fused(
                     codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho,
-                    out=o, ch_scale=sc, ch_shift=sh, workspace=None if mfma else ws,
-                    split_k=sp, config=cfg, kc_steps=layer.kc_steps)
+                    out=o, ch_scale=sc, ch_shift=sh, relu=True, codes_a=ca,
+                    quant_a=(0.05, 9, 3), workspace=None if mfma else ws,
+                    split_k=sp, config=cfg, kc_steps=layer.kc_steps,
+                    kc_chunk=getattr(layer, "kc_chunk", -1))
                 res[(cfg, sp)] = time_fn(fn, max(5, args.iters // 2))
         best = min(res, key=res.get)
         auto = res[(0, 0)]
