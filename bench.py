@@ -5,9 +5,10 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one TQ forward of one synthetic 256x3x224x224 batch per GPU (BASELINE.json
-configs[1]): the 19 converted convs run the term-pair kernel on HIP-encoded
-activations, everything else (stem conv, BN, ReLU, pooling, fc) is torch on the same
-stream.  Inputs are resident in HBM before timing.  Ranks run independent batches (weak
+configs[1]) through the fused executor (tq_fuse.py): the stem (conv, BN,
+ReLU, max-pool, first codes) is one HIP kernel, the 19 converted convs run the term-pair
+kernels with BN/residual/ReLU/next-layer TR in their epilogue; avgpool and fc are torch on
+the same stream.  Inputs are resident in HBM before timing.  Ranks run independent batches (weak
 scaling, no data-path collective); one all-reduce of the accuracy counters closes the
 timed region.  Rank 0 prints one JSON line.
 """
@@ -157,7 +158,36 @@ def cpu_baseline(model_fp, qmodel, nimg):
             "sample": "%d synthetic 3x224x224 images, ResNet-18 TQ forward: oracle TR "
                       "(oracle/tr_oracle.c, 1 thread) on every TR-layer activation + torch-CPU "
                       "fp32 conv (1 thread) on the fake-quantized tensors; weight TR excluded "
-                      "(one-time conversion)" % nimg}
+                      "(one-time conversion)" % nimg,
+            "tr_op": cpu_tr_op_baseline(oracle)}
+
+
+def cpu_tr_op_baseline(oracle, n=1 << 24):
+    """SURVEY 8(d) CPU baseline (iii): the TR op alone (D1: relu(N(0,1)) activations,
+    sf=0.05, db=9, dt=3, g=1) by the C oracle on 1 thread and on T host threads (chunks of the
+    flat tensor; elements are independent at g=1 and ctypes releases the GIL), elements/s.
+    T = OMP_NUM_THREADS (16 on the GPU box: its CPU share), else the visible core count."""
+    from concurrent.futures import ThreadPoolExecutor
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    x = np.maximum(np.random.default_rng(0).standard_normal(n, dtype=np.float32), 0)
+
+    def run(chunk):
+        return oracle.tr(chunk.reshape(1, -1, 1, 1), 0.05, DB, 1, DT)
+
+    small = x[: n // 8]
+    t0 = time.perf_counter()
+    run(small)
+    t1 = time.perf_counter() - t0
+    chunks = np.array_split(x, threads * 4)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, chunks[:threads]))  # warm the pool
+        t0 = time.perf_counter()
+        list(ex.map(run, chunks))
+        tn = time.perf_counter() - t0
+    return {"elements_per_s_1thread": small.size / t1, "elements_per_s": n / tn,
+            "threads": threads, "kind": "port",
+            "sample": "%d relu(N(0,1)) fp32 elements, TR g=1 (sf=0.05, db=9, dt=3), "
+                      "oracle/tr_oracle.c" % n}
 
 
 def main():
