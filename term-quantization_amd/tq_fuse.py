@@ -56,8 +56,10 @@ class _Conv(object):
         self.quant = (layer.input_quant.sf, layer.data_bits, layer.data_terms)
         self.scale, self.shift = _fold_bn(layer, bn)
         self.code_dtype = layer.w_codes.dtype   # int16 (VALU engine) / float16 (MFMA engine)
-        self.kc_steps = layer.kc_steps
-        self.kc_chunk = layer.kc_chunk
+        # every code tensor of the executor is TR of a ReLU output (the stem and the conv
+        # epilogues all apply ReLU before encoding), so the non-negative windows hold
+        self.kc_steps = layer.kc_steps_nonneg
+        self.kc_chunk = layer.kc_chunk_nonneg
         if self.cout % 4:
             raise ValueError("fused epilogue needs Cout % 4 == 0")
 

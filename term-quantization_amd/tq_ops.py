@@ -155,7 +155,31 @@ def pack_conv_weight(codes, engine="valu"):
     return packed.contiguous(), cp
 
 
-def mfma_flush_steps(packed, data_bits):
+def _window_sums(steps, nonneg):
+    """Per-window magnitude bounds from per-K-step code sums v [..., S, 64]: sum|v| in
+    general; max(sum of positive v, sum of |negative v|) when the activation codes are known
+    to be non-negative (post-ReLU): every partial sum of v_x * v_w with 0 <= v_x <= 2^db then
+    lies in [-2^db * N, 2^db * P], in any association order."""
+    if nonneg:
+        return [steps.clamp(min=0).sum(-1), (-steps).clamp(min=0).sum(-1)]
+    return [steps.abs().sum(-1)]
+
+
+def _longest_window(parts, lim, dim):
+    """Largest n such that every window of n consecutive steps along ``dim`` of every part
+    sums to at most lim (0 if none)."""
+    s = parts[0].shape[dim]
+    cs = [torch.nn.functional.pad(p.cumsum(dim), (1, 0)) for p in parts]
+    best = 0
+    for n in range(1, s + 1):
+        if max((c.narrow(dim, n, s + 1 - n) - c.narrow(dim, 0, s + 1 - n)).max().item()
+               for c in cs) > lim:
+            break
+        best = n
+    return best, s
+
+
+def mfma_flush_steps(packed, data_bits, nonneg=False):
     """Exactness window of the MFMA engine for fp16 weight codes ``packed`` [O_pad, Kp]
     against activation codes of ``data_bits`` bits (|v_x| <= 2^data_bits).
 
@@ -163,17 +187,11 @@ def mfma_flush_steps(packed, data_bits):
     row satisfies 2^data_bits * sum|v_w| <= 2^24 -- then every fp32 partial sum inside the
     window is an exact integer -- as the kernel's flush interval: 0 if the whole K range
     qualifies (no flush needed), -1 if not even one K-step does (the layer must use the VALU
-    engine)."""
+    engine).  ``nonneg``: the bound for non-negative activation codes (_window_sums)."""
     o_pad, kp = packed.shape
-    steps = packed.double().abs().view(o_pad, kp // K_ALIGN_MFMA, K_ALIGN_MFMA).sum(-1)
-    s = steps.shape[1]
+    steps = packed.double().view(o_pad, kp // K_ALIGN_MFMA, K_ALIGN_MFMA)
     lim = float(FP32_EXACT) / float(2**int(data_bits))
-    c = torch.nn.functional.pad(steps.cumsum(1), (1, 0))  # [O_pad, S + 1]
-    best = 0
-    for n in range(1, s + 1):
-        if (c[:, n:] - c[:, :s + 1 - n]).max().item() > lim:
-            break
-        best = n
+    best, s = _longest_window(_window_sums(steps, nonneg), lim, 1)
     if best == 0:
         return -1
     return 0 if best == s else best
@@ -205,26 +223,21 @@ def pack_stem_weight(w):
     return torch.stack([w0, w1]).contiguous().view(torch.int16)
 
 
-def mfma_flush_chunk(packed, data_bits, cp, ntaps):
+def mfma_flush_chunk(packed, data_bits, cp, ntaps, nonneg=False):
     """mfma_flush_steps for kernels that walk K chunk-major (tq.h ``kc_chunk``): the largest
     n such that every window of n consecutive filter taps of one 64-code channel chunk
     satisfies 2^data_bits * sum|v_w| <= 2^24 in every row; 0 if a whole chunk qualifies
     (the kernel also flushes at every chunk end), -1 if not even one step does or if Cp is
     not a multiple of 64 (no chunk-major kernel runs then; -1 lets the library derive a
-    conservative value from kc_steps)."""
+    conservative value from kc_steps).  ``nonneg`` as in mfma_flush_steps."""
     if cp % K_ALIGN_MFMA:
         return -1
     o_pad, kp = packed.shape
     nch = cp // K_ALIGN_MFMA
-    steps = packed.double().abs().view(o_pad, kp // K_ALIGN_MFMA, K_ALIGN_MFMA).sum(-1)
-    steps = steps[:, :ntaps * nch].reshape(o_pad, ntaps, nch).permute(0, 2, 1)  # [O, c, tap]
+    steps = packed.double().view(o_pad, kp // K_ALIGN_MFMA, K_ALIGN_MFMA)
+    steps = steps[:, :ntaps * nch].reshape(o_pad, ntaps, nch, K_ALIGN_MFMA).permute(0, 2, 1, 3)
     lim = float(FP32_EXACT) / float(2**int(data_bits))
-    c = torch.nn.functional.pad(steps.cumsum(2), (1, 0))  # [O, nch, ntaps + 1]
-    best = 0
-    for n in range(1, ntaps + 1):
-        if (c[:, :, n:] - c[:, :, :ntaps + 1 - n]).max().item() > lim:
-            break
-        best = n
+    best, _ = _longest_window(_window_sums(steps, nonneg), lim, 2)  # [O, c, tap] windows
     if best == 0:
         return -1
     return 0 if best == ntaps else best

@@ -219,8 +219,15 @@ class TRConv2dLayer(nn.Module):
             elif mode == "termpair":
                 packed, cp, self.engine, self.kc_steps = _pack_termpair(codes, data_bits,
                                                                         weight_bits)
-                self.kc_chunk = _kc_chunk(packed, self.engine, data_bits, cp,
-                                          codes.shape[2] * codes.shape[3])
+                ntaps = codes.shape[2] * codes.shape[3]
+                self.kc_chunk = _kc_chunk(packed, self.engine, data_bits, cp, ntaps)
+                # wider windows for callers whose activation codes are post-ReLU (>= 0): the
+                # fused executor (tq_fuse.py); the module path keeps the general windows
+                self.kc_steps_nonneg, self.kc_chunk_nonneg = self.kc_steps, self.kc_chunk
+                if self.engine == "mfma":
+                    self.kc_steps_nonneg = tq_ops.mfma_flush_steps(packed, data_bits, True)
+                    self.kc_chunk_nonneg = tq_ops.mfma_flush_chunk(packed, data_bits, cp,
+                                                                   ntaps, True)
             else:
                 packed, cp = tq_ops.pack_dw_weight(codes)
         else:
@@ -229,6 +236,7 @@ class TRConv2dLayer(nn.Module):
         self.termpair = mode == "termpair"
         if not self.termpair:
             self.engine, self.kc_steps, self.kc_chunk = None, 0, 0
+            self.kc_steps_nonneg, self.kc_chunk_nonneg = 0, 0
         self.register_buffer('w_codes', packed)
         if packed is not None:
             self.act_channels = cp

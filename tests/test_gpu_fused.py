@@ -208,6 +208,20 @@ def test_schedules_are_bit_identical(layer, cfgs, monkeypatch):
                                         quant_a=(0.05, 9, 3), config=cfg,
                                         kc_steps=lay_m.kc_steps)
         outs.append((o.cpu(), ca.cpu().to(torch.int16)))
+    # the wider exactness windows for non-negative (post-ReLU) codes, as the fused executor
+    # runs them: still the exact integer sums
+    for cfg in range(0, tq_native.lib().tq_conv2d_mfma_num_configs() + 1):
+        o = torch.full((batch, cout, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.zeros((batch, ho, ho, tq_ops.act_channels(cout)), dtype=torch.float16,
+                         device=DEV)
+        tq_native.conv2d_termpair_fused(codes_m, lay_m.w_codes, cout, k, k, (s, s),
+                                        (k // 2, k // 2), (1, 1), ho, ho, out=o, ch_scale=sc,
+                                        ch_shift=sh, relu=True, codes_a=ca,
+                                        quant_a=(0.05, 9, 3), config=cfg,
+                                        kc_steps=lay_m.kc_steps_nonneg,
+                                        kc_chunk=lay_m.kc_chunk_nonneg)
+        outs.append((o.cpu(), ca.cpu().to(torch.int16)))
     o0, c0 = outs[0]
     assert not torch.isnan(o0).any()
     for o, c in outs[1:]:

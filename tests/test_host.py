@@ -389,3 +389,32 @@ def test_relu_fast_path_restatement():
         got = (pos & keep) - (neg & keep)
         exp = oracle.tr(y.reshape(1, -1, 1, 1), float(sf), bw, 1, k).reshape(-1) / sf
         np.testing.assert_array_equal(got.astype(np.float64), np.round(exp.astype(np.float64)))
+
+
+def test_mfma_flush_nonneg_windows():
+    """tq_ops.mfma_flush_steps(nonneg=True) against its spec by brute force: the largest n
+    with max(sum of positive v_w, sum of |negative v_w|) * 2^db <= 2^24 over every window of
+    n K-steps of every row; never narrower than the general (sum |v_w|) window."""
+    import tq_ops  # noqa: F811
+    g = torch.Generator().manual_seed(3)
+    for trial in range(6):
+        o, steps = 5, 12
+        v = torch.randint(-256, 257, (o, steps * 64), generator=g).double()
+        if trial % 2:
+            v[:, : steps * 32] = v[:, : steps * 32].abs()  # sign-skewed rows
+        db = 9
+        lim = 2.0**24 / 2**db
+        st = v.view(o, steps, 64)
+        pos, neg = st.clamp(min=0).sum(-1), (-st).clamp(min=0).sum(-1)
+
+        def ok(n):
+            return all(max(float(pos[r, i:i + n].sum()), float(neg[r, i:i + n].sum())) <= lim
+                       for r in range(o) for i in range(steps - n + 1))
+        best = max([n for n in range(1, steps + 1) if ok(n)], default=0)
+        exp = -1 if best == 0 else (0 if best == steps else best)
+        got = tq_ops.mfma_flush_steps(v, db, nonneg=True)
+        assert got == exp, (trial, got, exp)
+        gen = tq_ops.mfma_flush_steps(v, db)
+        assert gen != -1 or got == -1
+        if gen > 0:
+            assert got == 0 or got >= gen
