@@ -172,7 +172,10 @@ int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int
  * Kernels that walk K chunk-major (the input-patch engine: for each 64-code channel chunk,
  * all filter taps) use `kc_chunk` instead: the same bound over every window of kc_chunk
  * consecutive taps of one chunk (0 = never needed; -1 = derive a conservative value from
- * kc_steps); they also flush at every chunk end.
+ * kc_steps); they also flush at every chunk end.  When every act_code is >= 0 (TR of a ReLU
+ * output) the window bound may use max(sum of positive w_codes, sum of |negative w_codes|)
+ * in place of sum |w_codes|: every partial sum then lies between -max_act * neg and
+ * max_act * pos (tq_ops.mfma_flush_steps(..., nonneg=True)).
  *   act_codes  [n][h][w][cp] fp16 codes, 16-byte aligned
  *   w_codes    [cout_pad][kp] fp16 codes, cout_pad a multiple of tq_conv2d_cout_align(),
  *              kp a multiple of 64
