@@ -144,8 +144,8 @@ def sweep(args, dev):
                     codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho,
                     out=o, ch_scale=sc, ch_shift=sh, relu=True, codes_a=ca,
                     quant_a=(0.05, 9, 3), workspace=None if mfma else ws,
-                    split_k=sp, config=cfg, kc_steps=layer.kc_steps,
-                    kc_chunk=getattr(layer, "kc_chunk", -1))
+                    split_k=sp, config=cfg, kc_steps=layer.kc_steps_nonneg,
+                    kc_chunk=layer.kc_chunk_nonneg)  # relu'd inputs, as the fused executor
                 res[(cfg, sp)] = time_fn(fn, max(5, args.iters // 2))
         best = min(res, key=res.get)
         auto = res[(0, 0)]
