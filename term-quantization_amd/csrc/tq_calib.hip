@@ -18,6 +18,9 @@ constexpr int kCalibThreads = 256;
 __global__ __launch_bounds__(kCalibThreads) void mse_profile_kernel(
     const float* __restrict__ x, const float* __restrict__ hist, int nbins,
     const float* __restrict__ sfs, float maxv, int k, double* __restrict__ errs) {
+  // no fma contraction: the reference materialises xh = tr(x) as a tensor and then computes
+  // x - xh, two roundings (a contracted x - v*sf would skip xh's rounding)
+#pragma clang fp contract(off)
   __shared__ double part[kCalibThreads];
   const float sf = sfs[blockIdx.x];
   double acc = 0.0;

@@ -5,8 +5,9 @@
 
 Same CLI and result JSON (accs, tmacs, param_bits).  The reference's profiling call passes
 ``input_shape=`` to get_model_ops and crashes (evaluate_mlp.py:88 vs profile_model.py:51);
-here it passes a 1x1x28x28 input as intended.  Like the reference, TR layers need the GPU
-(the TR op rejects CPU tensors); ``--no-cuda`` therefore fails at conversion.
+here it passes a 1x1x28x28 input as intended.  ``--no-cuda`` (BASELINE configs[0]) runs the
+TR layers on CPU tensors through the host TR op (libtq_host.so, include/tq_host.h) -- the
+reference's CPU run would fail there, since its extension rejects CPU tensors.
 """
 import argparse
 import json

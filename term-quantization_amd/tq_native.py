@@ -1,9 +1,11 @@
 """ctypes binding of libtq_hip.so (include/tq.h) for torch tensors.
 
-This is the only place the Python host layer touches native code.  The library is built
+This is the only place the Python host layer touches native code.  The libraries are built
 in-tree (``make -C term-quantization_amd`` or ``__graft_entry__.build()``) and loaded from
-``term-quantization_amd/lib/libtq_hip.so``; if it is missing every op raises -- there is no
-CPU or PyTorch fallback for the TQ path.
+``term-quantization_amd/lib/``: ``libtq_hip.so`` (include/tq.h, the MI355X kernels) for CUDA
+tensors and ``libtq_host.so`` (include/tq_host.h, the OpenMP CPU TR op) for CPU tensors.  If the
+library a call needs is missing it raises -- there is no PyTorch fallback, and a CUDA tensor
+never runs on the host library.
 
 Every call enqueues on torch's current HIP stream of the tensor's device, so the ops order
 correctly with surrounding torch work and can be captured into a CUDA/HIP graph.
@@ -17,8 +19,10 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TQ_LIB_PATH: an alternative in-tree build of the same library (tools: ablation builds)
 LIB_PATH = os.environ.get("TQ_LIB_PATH") or os.path.join(_HERE, "lib", "libtq_hip.so")
+HOST_LIB_PATH = os.path.join(_HERE, "lib", "libtq_host.so")
 
 _lib = None
+_host_lib = None
 _lock = threading.Lock()
 
 _i64 = ctypes.c_int64
@@ -117,6 +121,78 @@ def lib():
                     fn.restype = _RESTYPE.get(name, ctypes.c_int)
                 _lib = l
     return _lib
+
+
+# include/tq_host.h: name -> argtypes (int status unless in _HOST_RESTYPE)
+_HOST_SIGNATURES = {
+    "tq_host_version": [],
+    "tq_host_last_error": [],
+    "tq_tr_f32_host": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _i32],
+    "tq_tr_f64_host": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _i32],
+    "tq_tr_encode_f32_host": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32,
+                              _i32, _i32],
+    "tq_mse_profile_host": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _i32],
+}
+_HOST_RESTYPE = {"tq_host_version": ctypes.c_char_p, "tq_host_last_error": ctypes.c_char_p}
+HOST_EXPORTED_SYMBOLS = tuple(_HOST_SIGNATURES)
+
+
+def host_lib():
+    """Load libtq_host.so (the CPU TR op) once; raise if it has not been built."""
+    global _host_lib
+    if _host_lib is None:
+        with _lock:
+            if _host_lib is None:
+                if not os.path.exists(HOST_LIB_PATH):
+                    raise NativeLibraryMissing(
+                        "term-quantization host library not found at %s; build it with "
+                        "`make -C term-quantization_amd`" % HOST_LIB_PATH)
+                l = ctypes.CDLL(HOST_LIB_PATH)
+                for name, argtypes in _HOST_SIGNATURES.items():
+                    fn = getattr(l, name)
+                    fn.argtypes = argtypes
+                    fn.restype = _HOST_RESTYPE.get(name, ctypes.c_int)
+                _host_lib = l
+    return _host_lib
+
+
+def _check_host(rc):
+    if rc != 0:
+        raise RuntimeError(host_lib().tq_host_last_error().decode())
+
+
+def _host_threads():
+    return int(torch.get_num_threads())
+
+
+def tr_into_host(inp, out, sf, bitwidth, group_size, num_keep_terms, codes=None):
+    """The TR op on contiguous CPU tensors (tq_tr_*_host); OpenMP with torch's intra-op
+    thread count.  ctypes drops the GIL for the call."""
+    shape = (_i64 * inp.dim())(*inp.shape)
+    nt = _host_threads()
+    if codes is not None:
+        rc = host_lib().tq_tr_encode_f32_host(_ptr(inp), _ptr(out), _ptr(codes), inp.dim(),
+                                              shape, sf, bitwidth, group_size, num_keep_terms,
+                                              nt)
+    elif inp.dtype == torch.float32:
+        rc = host_lib().tq_tr_f32_host(_ptr(inp), _ptr(out), inp.dim(), shape, sf, bitwidth,
+                                       group_size, num_keep_terms, nt)
+    else:
+        rc = host_lib().tq_tr_f64_host(_ptr(inp), _ptr(out), inp.dim(), shape, sf, bitwidth,
+                                       group_size, num_keep_terms, nt)
+    _check_host(rc)
+    return out
+
+
+def mse_profile_host(x, hist, sfs, bitwidth, num_keep_terms):
+    """errs[s] (float64, CPU) for each candidate scale in sfs (tq_mse_profile_host): the same
+    values, in the same summation order, as mse_profile on the GPU."""
+    errs = torch.empty(sfs.numel(), dtype=torch.float64)
+    rc = host_lib().tq_mse_profile_host(_ptr(x), _ptr(hist), x.numel(), _ptr(sfs), sfs.numel(),
+                                        int(bitwidth), int(num_keep_terms), _ptr(errs),
+                                        _host_threads())
+    _check_host(rc)
+    return errs
 
 
 def version():

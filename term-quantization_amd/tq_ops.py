@@ -13,8 +13,13 @@ v_dot2c_i32_i16) and the MFMA engine (fp16 codes, v_mfma_f32_32x32x16_f16 with e
 windows flushed into int32, csrc/tr_conv_mfma.hip).  Their outputs are bit-identical; a
 layer uses MFMA when its codes fit fp16 exactly (bitwidths <= 11) unless TQ_CONV_ENGINE=valu.
 
-Errors mirror the reference boundary (kernels/tr_cuda.cpp:12-18): RuntimeError for a non-CUDA
-or non-contiguous input, a RuntimeError for an unsupported dtype, IndexError for < 2 dims.
+The TR ops (tr, tr_elementwise, tr_encode) take CUDA tensors (libtq_hip.so) and, as the
+deliberate extension of SURVEY.md 8(b), CPU tensors (libtq_host.so, the OpenMP host TR op --
+bit-identical results; the reference rejects CPU tensors and so cannot run its own MNIST CPU
+config).  The term-pair conv/linear ops are GPU-only.
+Errors mirror the reference boundary (kernels/tr_cuda.cpp:12-18): RuntimeError for a tensor on
+any other device or a non-contiguous input, a RuntimeError for an unsupported dtype,
+IndexError for < 2 dims.
 """
 import numpy as np
 import torch
@@ -48,8 +53,8 @@ def _check_input(input):
     # kernels/tr_cuda.cpp:12-18 (CHECK_CUDA, CHECK_CONTIGUOUS) and the dispatch dtype check
     if not isinstance(input, torch.Tensor):
         raise TypeError("tr(): input must be a torch.Tensor")
-    if not input.is_cuda:
-        raise RuntimeError("input must be a CUDA tensor")
+    if input.device.type not in ("cuda", "cpu"):
+        raise RuntimeError("input must be a CUDA (or CPU) tensor")
     if not input.is_contiguous():
         raise RuntimeError("input must be contiguous")
     if input.dtype not in (torch.float32, torch.float64):
@@ -70,8 +75,8 @@ def tr(input, sf, bitwidth, group_size, num_keep_terms):
     out = torch.empty_like(input, memory_format=torch.contiguous_format)
     if input.numel() == 0:
         return out
-    return tq_native.tr_into(input, out, float(sf), int(bitwidth), int(group_size),
-                             int(num_keep_terms))
+    run = tq_native.tr_into if input.is_cuda else tq_native.tr_into_host
+    return run(input, out, float(sf), int(bitwidth), int(group_size), int(num_keep_terms))
 
 
 def tr_elementwise(x, sf, bitwidth, num_keep_terms):
@@ -79,8 +84,8 @@ def tr_elementwise(x, sf, bitwidth, num_keep_terms):
 
     Elementwise, so a channels_last (or otherwise permuted but dense) tensor is processed in
     its own memory order and the result keeps the input's strides."""
-    if not x.is_cuda:
-        raise RuntimeError("input must be a CUDA tensor")
+    if x.device.type not in ("cuda", "cpu"):
+        raise RuntimeError("input must be a CUDA (or CPU) tensor")
     if x.dtype not in (torch.float32, torch.float64):
         raise RuntimeError('"tr_cuda" not implemented for \'%s\'' % str(x.dtype))
     if x.is_contiguous():
@@ -103,8 +108,8 @@ def tr_encode(w, sf, bitwidth, group_size, num_keep_terms):
     codes = torch.empty(w.shape, dtype=torch.int32, device=w.device)
     if w.numel() == 0:
         return out, codes
-    tq_native.tr_into(w, out, float(sf), int(bitwidth), int(group_size), int(num_keep_terms),
-                      codes=codes)
+    run = tq_native.tr_into if w.is_cuda else tq_native.tr_into_host
+    run(w, out, float(sf), int(bitwidth), int(group_size), int(num_keep_terms), codes=codes)
     return out, codes
 
 

@@ -79,12 +79,14 @@ def mse_profile(hist, minv, maxv, bit_width, terms):
     Same candidate grid (2048 fp32 sfs in linspace(1e-8, maxv)) and the same histogram grid
     as the reference; all 2048 candidates are scored in one HIP launch (tq_mse_profile) and
     the first arg-min is returned as a Python float, like ``sfs[min_idx]``."""
-    device = hist.device if hist.is_cuda else torch.device("cuda")
+    device = hist.device
     x = torch.linspace(minv, maxv, len(hist)).to(device)
     sfs_list = torch.linspace(1e-8, maxv, 2048).tolist()
     sfs = torch.tensor(sfs_list, dtype=torch.float32, device=device)
     h = hist.detach().to(device=device, dtype=torch.float32).contiguous()
-    errs = tq_native.mse_profile(x.contiguous(), h, sfs, bit_width, terms)
+    # the HIP kernel for a GPU histogram, the host library (same errs) for a CPU one
+    run = tq_native.mse_profile if hist.is_cuda else tq_native.mse_profile_host
+    errs = run(x.contiguous(), h, sfs, bit_width, terms)
     min_idx = int(torch.argmin(errs).item())
     return sfs_list[min_idx]
 
@@ -184,7 +186,10 @@ class TRConv2dLayer(nn.Module):
                    (int16 codes, ``self.engine`` "valu") -- bit-identical results
       "depthwise"  groups == C_in == C_out, weight bits <= 22: tq_ops.tr_dwconv2d
       "reference"  anything else: the reference composition self.conv(self.input_quant(x))
-                   with the HIP TR op (``self.termpair`` is True only for "termpair")."""
+                   with the HIP TR op (``self.termpair`` is True only for "termpair").
+    The term-pair kernels are GPU kernels: a CPU input (the MNIST CPU config)
+    runs the reference composition with the host TR op (libtq_host.so) and torch's CPU conv
+    on the same TR'd weights.  A CUDA input never takes that path."""
 
     def __init__(self, conv_layer, data_bits=8, data_terms=4, weight_bits=8,
                  group_size=1, num_terms=8):
@@ -244,7 +249,7 @@ class TRConv2dLayer(nn.Module):
         self.conv = conv_layer
 
     def forward(self, x):
-        if self.input_quant.tracking or self.mode == "reference":
+        if self.input_quant.tracking or self.mode == "reference" or not x.is_cuda:
             xq = self.input_quant(x)
             return self.conv(xq)
         c = self.conv
@@ -319,7 +324,7 @@ class TRLinearLayer(nn.Module):
             return self.linear(x)
         if not self.quantize_input:
             return self.linear(x)
-        if not self.termpair:
+        if not self.termpair or not x.is_cuda:  # CPU input: host TR + torch's CPU linear
             return self.linear(self.input_quant(x))
         return tq_ops.tr_linear(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, self.linear.bias,

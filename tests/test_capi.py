@@ -105,8 +105,9 @@ def test_conv_f16_argument_validation():
     assert lib.tq_conv2d_mfma_num_configs() >= 1
 
 
-def test_ops_reject_cpu_tensors_like_the_reference():
+def test_ops_reject_other_devices_like_the_reference():
+    # CPU tensors run on the host library (tests/test_host_tr.py); anything else is refused
     with pytest.raises(RuntimeError, match="CUDA"):
-        tq_ops.tr(torch.zeros(2, 4), 1.0, 8, 1, 1)
+        tq_ops.tr(torch.zeros(2, 4, device="meta"), 1.0, 8, 1, 1)
     with pytest.raises(RuntimeError, match="CUDA"):
-        tq_ops.tr_elementwise(torch.zeros(2, 4), 1.0, 8, 1)
+        tq_ops.tr_elementwise(torch.zeros(2, 4, device="meta"), 1.0, 8, 1)

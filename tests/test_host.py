@@ -2,8 +2,8 @@
 counter against the reference's published results/*.json, calibration bookkeeping.
 
 TR layers are built on CPU with the TR op replaced by a stand-in (the oracle, or an
-identity stub where only shapes matter) -- the product's TR op requires a HIP device,
-exactly as the reference's does."""
+identity stub where only shapes matter) so these tests isolate the host logic; the product's
+own CPU TR op (libtq_host.so) is tested in test_host_tr.py."""
 import json
 import os
 
