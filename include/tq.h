@@ -111,12 +111,13 @@ int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w
  *                                                       eval-mode BatchNorm folded, fp64)
  *     = fp32(acc * scale + bias[c])                    otherwise (plain conv)
  *   y = y + residual[p][c]            (fp32, if residual; [P][cout] channels_last)
- *   y = max(y, 0)                     (if relu)
+ *   y = max(y, 0)                     (if relu; the stored out keeps a NaN, as torch.relu)
  *   out[p][c] = y                     (if out)
  *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   format fmt_a, [P][cp_a] (if codes_a)
  *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   format fmt_b, [P][cp_b] (if codes_b)
  * codes_a/_b are the next TR layers' activation codes (tr_layer.py:96-99 applied to y), so
- * those layers skip their own activation pass.  cp_* = roundup(cout, 8); cout % 4 == 0.
+ * those layers skip their own activation pass.  cp_* = roundup(cout, 8); cout % 4 == 0; the
+ * pad channels [cout, cp_*) of codes_a/_b are written as zero codes.
  */
 typedef struct tq_conv_epilogue {
   const double *ch_scale;
@@ -165,9 +166,10 @@ int tq_conv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int
 /*
  * Term-pair Conv2d (groups = 1) on the matrix cores: the same exact integer sums as
  * tq_conv2d_termpair(_fused), from fp16 codes (TQ_CODES_F16) with v_mfma_f32_32x32x16_f16.
- * fp32 accumulators are exact while every partial sum stays below 2^24; the caller passes
+ * fp32 accumulators are exact while every partial sum stays within 2^24 in magnitude (2^24
+ * itself is an fp32 value, so every such partial sum is an exact integer); the caller passes
  * `kc_steps` >= 1 such that for every weight row m and every window of kc_steps K-steps of
- * 64 codes, max|act_code| * sum_{k in window} |w_codes[m][k]| < 2^24 (0 = the whole K
+ * 64 codes, max|act_code| * sum_{k in window} |w_codes[m][k]| <= 2^24 (0 = the whole K
  * range satisfies it), and max_m sum_k |w_codes[m][k]| * max|act_code| < 2^31.
  * Kernels that walk K chunk-major (the input-patch engine: for each 64-code channel chunk,
  * all filter taps) use `kc_chunk` instead: the same bound over every window of kc_chunk

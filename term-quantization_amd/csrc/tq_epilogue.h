@@ -5,7 +5,8 @@
 //   y = fp32(double(acc) * ch_scale[c] + ch_shift[c])   (conv scale, bias, folded eval BN)
 //     | fp32(double(acc) * scale + bias[c])
 //   y += residual (fp32), relu, fp32 store, next TR layers' activation codes
-//   (tr_layer.py:96-99 applied to y) in the consumer's code format.
+//   (tr_layer.py:96-99 applied to y) in the consumer's code format.  ReLU propagates NaN
+//   into the stored value as torch.relu does; the codes of a NaN are 0, as TR(NaN) = 0.
 #pragma once
 
 #include "tq_device.h"
@@ -30,7 +31,11 @@ __device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4
   }
 }
 
-__device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, int co,
+// Codes of channels co..co+3 of pixel p.  The lane owning the last quad (co + 4 == cout) also
+// zeroes the pad channels [cout, cp) (cp = roundup(cout, 8), so at most 4): a consumer
+// multiplies them by zero weights, and stale fp16 bits decoding as Inf/NaN would turn 0 * Inf
+// into NaN in its fp32 window.
+__device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, int64_t p, int co,
                                              const float y[4], double inv_sf, float maxv,
                                              int k, int fmt, bool relu) {
   uint32_t v[4];
@@ -45,6 +50,7 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int64_t p, 
   }
   *reinterpret_cast<int2*>(codes + p * cp + co) =
       make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+  if (co + 4 == cout && cp > cout) *reinterpret_cast<int2*>(codes + p * cp + co + 4) = make_int2(0, 0);
 }
 
 // emit4_nhwc with the residual already loaded (rv = residual[p][co..co+3], or zeros when
@@ -62,15 +68,20 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
     y[2] += rv.z;
     y[3] += rv.w;
   }
-  if (a.relu) {
+  float o[4];  // stored value: ReLU keeps NaN like torch.relu; the codes see 0 (TR(NaN) = 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+  for (int i = 0; i < 4; ++i) {
+    o[i] = y[i];
+    if (a.relu) {
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      o[i] = o[i] != o[i] ? o[i] : y[i];
+    }
   }
   if (a.out)
-    *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(y[0], y[1], y[2], y[3]);
-  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
+    *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(o[0], o[1], o[2], o[3]);
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
                                a.relu);
-  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
                                a.relu);
 }
 
@@ -97,23 +108,28 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
         if (co + i < a.Cout) y[i] += r[i];
     }
   }
-  if (a.relu) {
+  float o[4];  // as emit4_nhwc_res: NaN-propagating ReLU for the stored value
 #pragma unroll
-    for (int i = 0; i < 4; ++i) y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+  for (int i = 0; i < 4; ++i) {
+    o[i] = y[i];
+    if (a.relu) {
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      o[i] = o[i] != o[i] ? o[i] : y[i];
+    }
   }
   if (a.out) {
     float* dst = a.out + p * a.Cout + co;
     if (vec) {
-      *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
+      *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (co + i < a.Cout) dst[i] = y[i];
+        if (co + i < a.Cout) dst[i] = o[i];
     }
   }
-  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
+  if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
                                a.relu);
-  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
+  if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
                                a.relu);
 }
 

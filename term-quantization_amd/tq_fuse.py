@@ -42,7 +42,7 @@ def _fold_bn(layer, bn):
 class _Conv(object):
     """One TRConv2dLayer prepared for the fused kernel."""
 
-    def __init__(self, layer, bn):
+    def __init__(self, layer, bn, nonneg=False):
         if not isinstance(layer, tr_layer.TRConv2dLayer) or not layer.termpair:
             raise ValueError("fused executor needs term-pair TRConv2dLayer convolutions")
         if layer.input_quant.tracking:
@@ -54,12 +54,14 @@ class _Conv(object):
         self.stride, self.padding, self.dilation = c.stride, c.padding, c.dilation
         self.cp_in = layer.act_channels
         self.quant = (layer.input_quant.sf, layer.data_bits, layer.data_terms)
+        self.bn = bn
         self.scale, self.shift = _fold_bn(layer, bn)
         self.code_dtype = layer.w_codes.dtype   # int16 (VALU engine) / float16 (MFMA engine)
-        # every code tensor of the executor is TR of a ReLU output (the stem and the conv
-        # epilogues all apply ReLU before encoding), so the non-negative windows hold
-        self.kc_steps = layer.kc_steps_nonneg
-        self.kc_chunk = layer.kc_chunk_nonneg
+        # nonneg: the caller guarantees the input codes are TR of a ReLU output (>= 0), so
+        # the wider non-negative exactness windows hold; otherwise the general ones
+        self.nonneg = bool(nonneg)
+        self.kc_steps = layer.kc_steps_nonneg if nonneg else layer.kc_steps
+        self.kc_chunk = layer.kc_chunk_nonneg if nonneg else layer.kc_chunk
         if self.cout % 4:
             raise ValueError("fused epilogue needs Cout % 4 == 0")
 
@@ -70,6 +72,9 @@ class _Conv(object):
                                      self.dilation[1]))
 
     def __call__(self, codes, out=None, residual=None, relu=False, next_a=None, next_b=None):
+        for nxt in (next_a, next_b):
+            if nxt is not None and nxt.nonneg and not relu:
+                raise ValueError("a consumer with non-negative windows needs ReLU'd codes")
         n, h, w, _ = codes.shape
         ho, wo = self.out_hw(h, w)
         dev = codes.device
@@ -110,11 +115,14 @@ def _same_codes(a, b):
 
 class _Block(object):
     def __init__(self, block):
-        self.conv1 = _Conv(block.conv1, block.bn1)
-        self.conv2 = _Conv(block.conv2, block.bn2)
+        # every code tensor of the executor is TR of a ReLU output: the stem and every conv
+        # epilogue that emits codes apply ReLU first (forward() asserts relu wherever codes are
+        # produced), so all three convs take the non-negative windows
+        self.conv1 = _Conv(block.conv1, block.bn1, nonneg=True)
+        self.conv2 = _Conv(block.conv2, block.bn2, nonneg=True)
         self.down = None
         if block.downsample is not None:
-            self.down = _Conv(block.downsample[0], block.downsample[1])
+            self.down = _Conv(block.downsample[0], block.downsample[1], nonneg=True)
 
 
 def _pool_params(mp):
@@ -218,26 +226,46 @@ class FusedResNet(nn.Module):
         return out, codes, codes_down
 
     @torch.no_grad()
-    def forward(self, x):
+    def forward(self, x, capture=None):
+        """Logits of a batch.  ``capture`` (a list, tests only) receives one record per
+        term-pair conv -- {"name", "conv", "codes_in", "residual", "out", "codes_a",
+        "codes_b"} -- plus a "stem" record, and makes every conv also store its fp32 output
+        (the epilogue computes it either way; the codes are identical)."""
         m = self.qmodel
+        keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
         x, codes, codes_down = self._stem(x)
+        if keep:
+            capture.append({"name": "stem", "out": x, "codes_a": codes, "codes_b": codes_down})
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
-            _, mid, _ = b.conv1(codes, relu=True, next_a=b.conv2)
+            y1, mid, _ = b.conv1(codes, out=True if keep else None, relu=True, next_a=b.conv2)
+            if keep:
+                capture.append({"name": "block%d.conv1" % i, "conv": b.conv1, "codes_in": codes,
+                                "residual": None, "out": y1, "codes_a": mid, "codes_b": None})
             if b.down is not None:
                 identity, _, _ = b.down(codes_down, out=True)
+                if keep:
+                    capture.append({"name": "block%d.downsample" % i, "conv": b.down,
+                                    "codes_in": codes_down, "residual": None, "out": identity,
+                                    "codes_a": None, "codes_b": None})
             else:
                 identity = x
             next_b = nxt.down if nxt is not None and nxt.down is not None else None
             shared = next_b is not None and _same_codes(nxt.conv1, next_b)
             # a block followed by a downsampling block: its fp32 output is nobody's residual
             # (the next identity is the downsample conv's), so only its codes are written
+            cin = mid
             x, codes, codes_down = b.conv2(
-                mid, out=True if next_b is None else None, residual=identity, relu=True,
-                next_a=nxt.conv1 if nxt else None, next_b=None if shared else next_b)
+                mid, out=True if (next_b is None or keep) else None, residual=identity,
+                relu=True, next_a=nxt.conv1 if nxt else None,
+                next_b=None if shared else next_b)
             if shared:
                 codes_down = codes
+            if keep:
+                capture.append({"name": "block%d.conv2" % i, "conv": b.conv2, "codes_in": cin,
+                                "residual": identity, "out": x, "codes_a": codes,
+                                "codes_b": codes_down})
         x = m.avgpool(x)
         x = torch.flatten(x, 1)
         return m.fc(x)

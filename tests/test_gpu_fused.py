@@ -1,5 +1,5 @@
-"""GPU parity of the fused term-pair epilogue (BN fold, residual, ReLU, next-layer TR codes)
-and of the fused ResNet executor against the module path."""
+"""GPU parity of the fused term-pair epilogue (BN fold, residual, ReLU, next-layer TR codes),
+its schedules and the stem tail."""
 import numpy as np
 import pytest
 import torch
@@ -76,32 +76,9 @@ def test_fused_epilogue_matches_reference_composition(cfg, engine):
     assert torch.equal(got, torch.from_numpy(exp_codes))
 
 
-@pytest.mark.parametrize("fused_stem", [False, True])
-def test_fused_resnet_matches_module_path(engine, fused_stem):
-    """With the module path's stem (MIOpen fp32 conv) the executors agree to the BN-fold
-    rounding.  The fused stem computes the same fp32-class conv in another summation order;
-    its ~1e-7 differences flip a few activation codes sitting on a quantization boundary,
-    and 17 quantized layers amplify those flips, so that comparison is looser (the stem
-    itself is checked against fp64 in test_gpu_stem.py)."""
-    torch.manual_seed(0)
-    model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
-    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
-    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
-    x = torch.randn(8, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
-    with torch.no_grad():
-        q(x)
-    tr_layer.set_tr_tracking(q, False)
-    fused = tq_fuse.FusedResNet(q)
-    if not fused_stem:
-        fused.stem_w = None
-    else:
-        assert fused.stem_w is not None
-    with torch.no_grad():
-        ref = q(x)
-        got = fused(x)
-    rel = (got - ref).norm() / ref.norm()
-    assert rel.item() < (2e-2 if fused_stem else 1e-3), rel.item()
-    assert (got.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.75
+# The executor-vs-module-path comparison lives in tests/test_gpu_fused_parity.py: teacher
+# forced, conv by conv, at the bench config (the former whole-network 2e-2 / 75 %-argmax
+# check could not tell an epilogue bug from rounding-midpoint code flips).
 
 
 @pytest.mark.parametrize("sf", [0.0, float("inf"), 1e-38, 1e30])

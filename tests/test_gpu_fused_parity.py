@@ -1,0 +1,219 @@
+"""Teacher-forced parity of the measured path: the fused ResNet-18 executor (tq_fuse.py) that
+bench.py times, at the bench config (BASELINE configs[1]: g=8, k=12, wb=db=9, dt=3, batch
+256 x 3 x 224 x 224, bench.py's calibration), checked conv by conv against the oracle.
+
+For every one of the 19 term-pair convs, on a sample of the batch's images:
+  (i)  its input codes are bit-exact oracle.tr() of the fp32 tensor they encode
+       (tr_layer.py:96-99: the producing epilogue's stored output, or the stem's), and the
+       channel padding holds zero codes;
+  (ii) its fp32 output is within 1e-5 of the fp64 composition conv -> BN -> (+ identity)
+       -> ReLU of those same codes (tr_layer.py:124-126 plus the torchvision block), with
+       the identity the kernel was handed.
+The capture mode only adds fp32 stores; the bench-mode logits must be bit-identical to it.
+
+A second test runs the module path (TRConv2dLayer + torch BN/ReLU/add, the reference
+composition) teacher-forced on the fused path's inputs: every activation-code mismatch
+between the two must be a one-step flip of the quantized integer whose two fp32 values sit
+within a few ulps of each other -- i.e. a rounding-midpoint straddle caused by the BN-fold
+rounding, never an indexing or epilogue bug."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import oracle
+import tq_fuse
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SAMPLE = [0, 131, 255]
+
+
+def _out(t, idx):
+    """Sample images of an fp32 [N, C, H, W] (channels_last) tensor, as fp64 NCHW."""
+    return t[idx].double().cpu().contiguous()
+
+
+def _codes(t, idx, c):
+    """Sample images of an NHWC [N, H, W, Cp] code tensor, first c channels, fp64 NCHW."""
+    return t[idx][..., :c].double().permute(0, 3, 1, 2).cpu().contiguous()
+
+
+def _tr_codes(y, quant):
+    """Integer term sums oracle.tr would produce for fp32 y (NCHW fp64 holding fp32 values)."""
+    sf, db, dt = quant
+    yq = oracle.tr(y.float().numpy().reshape(1, -1, 1, 1), sf, db, 1, dt).reshape(y.shape)
+    return np.rint(yq.astype(np.float64) / float(np.float32(sf))).astype(np.int64)
+
+
+def _reference(conv, codes_in, residual, idx, relu=True):
+    """fp64 conv -> BN -> (+residual) -> ReLU of the sampled input codes (teacher forced);
+    the downsample branch is conv -> BN only."""
+    layer = conv.layer
+    c = layer.conv
+    cin = c.in_channels
+    sf_x = float(np.float32(conv.quant[0]))
+    xq = _codes(codes_in, idx, cin) * sf_x
+    wq = c.weight.detach().double().cpu()  # TR(w) = v_w * sf_w exactly (fp32)
+    z = F.conv2d(xq, wq, None, c.stride, c.padding, c.dilation)
+    mag = F.conv2d(xq.abs(), wq.abs(), None, c.stride, c.padding, c.dilation)
+    if c.bias is not None:
+        z = z + c.bias.detach().double().cpu().view(1, -1, 1, 1)
+    bn = conv.bn
+    a = (bn.weight.detach().double() / torch.sqrt(bn.running_var.double() + bn.eps)).cpu()
+    y = (z - bn.running_mean.double().cpu().view(1, -1, 1, 1)) * a.view(1, -1, 1, 1) + \
+        bn.bias.detach().double().cpu().view(1, -1, 1, 1)
+    res = torch.zeros_like(y)
+    if residual is not None:
+        res = _out(residual, idx)
+        y = y + res
+    if relu:
+        y = torch.relu(y)
+    bound = 1e-5 * (torch.maximum(y.abs(), mag * a.abs().view(1, -1, 1, 1)) + res.abs()) + 1e-30
+    return y, bound
+
+
+def _check_input_codes(rec, src, idx):
+    conv = rec["conv"]
+    cin = conv.layer.conv.in_channels
+    got = rec["codes_in"][idx].long().cpu()
+    exp = _tr_codes(_out(src, idx), conv.quant)
+    assert torch.equal(got[..., :cin].permute(0, 3, 1, 2), torch.from_numpy(exp)), rec["name"]
+    if got.shape[-1] > cin:
+        assert not got[..., cin:].any(), rec["name"] + ": pad channels"
+
+
+@pytest.fixture(scope="module")
+def bench_model():
+    import os
+    import bench
+    old = os.environ.get("TQ_CONV_ENGINE")
+    os.environ["TQ_CONV_ENGINE"] = "mfma"
+    try:
+        dev = torch.device(DEV)
+        _, qmodel, _ = bench.build_model(dev, 256, 0)   # bench.py's model + calibration
+    finally:
+        if old is None:
+            os.environ.pop("TQ_CONV_ENGINE")
+        else:
+            os.environ["TQ_CONV_ENGINE"] = old
+    import util
+    x, _ = util.SyntheticImageNet(512, 256, seed=0, device=dev).batch(0)  # bench batch 0
+    return qmodel, x.contiguous(memory_format=torch.channels_last)
+
+
+def test_fused_executor_teacher_forced_at_bench_config(bench_model):
+    qmodel, x = bench_model
+    fused = tq_fuse.FusedResNet(qmodel)
+    assert fused.stem_w is not None  # the fused stem kernel, as in the bench
+    with torch.no_grad():
+        logits = fused(x)
+        rec = []
+        logits_cap = fused(x, capture=rec)
+    torch.cuda.synchronize()
+    assert torch.equal(logits, logits_cap)  # capture adds stores only
+    convs = [r for r in rec if r["name"] != "stem"]
+    assert len(convs) == 19
+    idx = SAMPLE
+    block_out = rec[0]["out"]  # fp32 tensor the next conv1 / downsample codes encode
+    conv1_out = None
+    for r in convs:
+        conv = r["conv"]
+        if r["name"].endswith("conv2"):
+            src = conv1_out
+        else:
+            src = block_out
+        _check_input_codes(r, src, idx)
+        y_ref, bound = _reference(conv, r["codes_in"], r["residual"], idx,
+                                  relu=not r["name"].endswith("downsample"))
+        y = _out(r["out"], idx)
+        err = (y - y_ref).abs()
+        assert bool((err <= bound).all()), "%s: max err / bound %.3g" % (
+            r["name"], float((err / bound).max()))
+        if r["name"].endswith("conv1"):
+            conv1_out = r["out"]
+        elif r["name"].endswith("conv2"):
+            block_out = r["out"]
+
+
+def _quantize(y, quant):
+    """q of kernels/tr_cuda_kernel.cu:21-23 for fp32 values y >= 0 (numpy)."""
+    sf, db, _ = quant
+    r = (np.abs(y.astype(np.float32)) / np.float32(sf)).astype(np.float32)
+    t = r.astype(np.float64) + 0.5
+    return np.minimum(np.floor(t), 2.0 ** db - 1).astype(np.int64)
+
+
+def test_module_path_teacher_forced_code_flips_are_midpoint_straddles(bench_model):
+    """The module path (reference composition: TRConv2dLayer forward, torch BN, ReLU, add)
+    and the fused executor fed the same inputs, layer by layer, on 8 images."""
+    qmodel, x = bench_model
+    x = x[:8].contiguous(memory_format=torch.channels_last)
+    fused = tq_fuse.FusedResNet(qmodel)
+    with torch.no_grad():
+        rec = []
+        fused(x, capture=rec)
+        # stem: module path = MIOpen conv + torch BN/ReLU/max-pool
+        m = qmodel
+        stem_mod = m.maxpool(m.relu(m.bn1(m.conv1(x))))
+        stem_fused = rec[0]["out"]
+        # (near-fp32 split-fp16 conv vs MIOpen fp32: both within ~1e-6 of fp64 relative to
+        # the products' magnitude; test_gpu_stem.py holds the per-element fp64 bound)
+        d = (stem_mod - stem_fused).abs().max().item()
+        assert d <= 1e-5 * stem_mod.abs().max().item(), d
+        # the per-block modules of the converted model, in executor order
+        blocks = [b for layer in (m.layer1, m.layer2, m.layer3, m.layer4) for b in layer]
+        convs = [r for r in rec if r["name"] != "stem"]
+        it = iter(convs)
+        block_in = stem_fused
+        flips = total = 0
+        for blk in blocks:
+            r1 = next(it)
+            y1_mod = blk.relu(blk.bn1(blk.conv1(block_in)))
+            pairs = [(r1, y1_mod, r1["out"], fused_next(rec, r1))]
+            if blk.downsample is not None:
+                rd = next(it)
+                identity = blk.downsample(block_in)
+                d = (identity - rd["out"]).abs().max().item()
+                assert d <= 1e-5 * (rd["out"].abs().max().item() + 1e-30), rd["name"]
+            r2 = next(it)
+            # teacher forced: conv2 sees the fused path's conv1 output and identity
+            y2_mod = blk.relu(blk.bn2(blk.conv2(r1["out"])) + r2["residual"])
+            pairs.append((r2, y2_mod, r2["out"], fused_next(rec, r2)))
+            for r, ym, yf, (codes, quant) in pairs:
+                ym = ym.contiguous(memory_format=torch.channels_last)
+                scale = yf.abs().amax().item() + 1e-30
+                assert (ym - yf).abs().max().item() <= 1e-5 * scale, r["name"]
+                if codes is None:
+                    continue
+                c = yf.shape[1]
+                got = codes[..., :c].long().cpu().permute(0, 3, 1, 2).numpy()
+                ymn = ym.float().cpu().numpy()
+                yfn = yf.float().cpu().numpy()
+                exp_mod = _tr_codes(torch.from_numpy(ymn).double(), quant)
+                assert np.array_equal(got, _tr_codes(torch.from_numpy(yfn).double(), quant))
+                mism = got != exp_mod
+                total += got.size
+                if not mism.any():
+                    continue
+                flips += int(mism.sum())
+                qm, qf = _quantize(ymn[mism], quant), _quantize(yfn[mism], quant)
+                assert np.all(np.abs(qm - qf) == 1), r["name"]
+                lo = np.minimum(qm, qf).astype(np.float64) + 0.5  # the straddled midpoint
+                sf = float(np.float32(quant[0]))
+                for v in (ymn[mism], yfn[mism]):
+                    ulp = np.spacing(np.abs(v).astype(np.float32)).astype(np.float64)
+                    assert np.all(np.abs(v.astype(np.float64) - lo * sf) <= 8 * ulp + lo * sf *
+                                  2.0 ** -22), r["name"]
+            block_in = r2["out"]
+        assert total > 0 and flips <= total * 1e-4, (flips, total)
+
+
+def fused_next(rec, r):
+    """(codes the fused conv emitted for its next consumer, that consumer's quantizer)."""
+    names = [q["name"] for q in rec]
+    i = names.index(r["name"])
+    for q in rec[i + 1:]:
+        if "conv" in q and q["codes_in"] is r["codes_a"]:
+            return r["codes_a"], q["conv"].quant
+    return None, None

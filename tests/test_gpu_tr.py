@@ -100,8 +100,9 @@ def test_tr_encode_codes_consistent():
 
 
 def test_tr_errors_mirror_reference():
+    # (CPU tensors are the host library's: tests/test_host_tr.py)
     with pytest.raises(RuntimeError, match="CUDA"):
-        tr_layer.tr_cuda.tr(torch.zeros(2, 2), 1.0, 8, 1, 1)
+        tr_layer.tr_cuda.tr(torch.zeros(2, 2, device="meta"), 1.0, 8, 1, 1)
     with pytest.raises(RuntimeError, match="contiguous"):
         tr_layer.tr_cuda.tr(torch.zeros(4, 4, device=DEV).t(), 1.0, 8, 1, 1)
     with pytest.raises(RuntimeError):
@@ -131,6 +132,22 @@ def test_tr_on_side_stream_orders_with_torch():
     torch.cuda.synchronize()
     exp = oracle.tr((x * 2).cpu().numpy(), 0.01, 9, 8, 12)
     assert torch.equal(z.cpu(), torch.from_numpy(exp))
+
+
+def test_mse_profile_device_equals_host():
+    """The calibration kernel and the host library sum the same fp32 per-bin errors in the
+    same fp64 order (no fma contraction on either side): identical errs, identical sf."""
+    import tq_native
+    torch.manual_seed(5)
+    hist = torch.histc(torch.relu(torch.randn(300000)) * 5, 8192, -50, 50)
+    x = torch.linspace(-50, 50, 8192)
+    sfs = torch.tensor(torch.linspace(1e-8, 50, 2048).tolist(), dtype=torch.float32)
+    for bits, terms in [(9, 3), (8, 8), (4, 2)]:
+        dev = tq_native.mse_profile(x.to(DEV), hist.to(DEV), sfs.to(DEV), bits, terms)
+        host = tq_native.mse_profile_host(x, hist, sfs, bits, terms)
+        assert torch.equal(dev.cpu(), host)
+        assert tr_layer.mse_profile(hist.to(DEV), -50, 50, bits, terms) == \
+            tr_layer.mse_profile(hist, -50, 50, bits, terms)
 
 
 def test_mse_profile_matches_oracle():

@@ -1,0 +1,142 @@
+"""Adversarial GPU checks of the MFMA engine's exactness windows and of the epilogue's code
+padding.
+
+* Weights whose window sums sit just under 2^24 / 2^db, with activation codes saturated at
+  maxv, so that a window one K-step wider than the host computed would carry an odd partial
+  sum above 2^24 (not an fp32 value).  Every MFMA tile config, run with the wider
+  non-negative windows (tq_ops.mfma_flush_steps / mfma_flush_chunk(nonneg=True)), must give
+  the VALU engine's exact int32 sums bit for bit.
+* Cout % 8 == 4: the fused epilogue must zero the pad channels of the codes it emits, so a
+  consumer never multiplies stale fp16 bits (Inf/NaN) by its zero pad weights."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import oracle
+import tq_native
+import tr_layer
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+SAT, ONE = 30, 1   # channels 0..29 at code 511, channel 30 at code 1, the rest 0
+
+
+def _weights(cin, cout):
+    """Codes +255 on channels < 32, -255 on channels >= 32 (rows < cout - 1); the last row
+    holds the single 256 that sets w_sf = max|w| / 2^8 so that 255 is a code."""
+    w = torch.zeros(cout, cin, 3, 3)
+    w[:cout - 1, :32] = 255.0
+    w[:cout - 1, 32:] = -255.0
+    w[cout - 1, 0, 0, 0] = 256.0
+    return w * 1e-3
+
+
+def _layer(cin, cout, stride, engine, monkeypatch):
+    monkeypatch.setenv("TQ_CONV_ENGINE", engine)
+    conv = nn.Conv2d(cin, cout, 3, stride, 0, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(_weights(cin, cout))
+    lay = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 9, 1, 9)  # g=1, k=9 keeps every term
+    assert lay.engine == engine
+    return lay
+
+
+def _act(n, cin, hw):
+    sf = 0.01
+    x = torch.zeros(n, cin, hw, hw)
+    x[:, :SAT] = 600 * sf       # saturates: q = 511 = 512 - 1 (two terms)
+    x[:, SAT:SAT + ONE] = sf    # q = 1
+    return x.to(DEV).contiguous(memory_format=torch.channels_last), sf
+
+
+@pytest.mark.parametrize("cout,stride,hw", [(64, 1, 12), (256, 1, 16), (256, 2, 17),
+                                            (128, 2, 15)])
+def test_nonneg_windows_at_the_bound(cout, stride, hw, monkeypatch):
+    cin, n = 64, 3
+    lay_m = _layer(cin, cout, stride, "mfma", monkeypatch)
+    codes_w = lay_m.w_codes[:cout - 1, :9 * 64].float()
+    assert bool((codes_w.abs() == 255).all())
+    # general window: 2^9 * 64 * 255 per K-step -> 2 steps; non-negative: 2^9 * 32 * 255 -> 4
+    assert lay_m.kc_steps == 2 and lay_m.kc_steps_nonneg == 4
+    assert lay_m.kc_chunk in (2, -1) and lay_m.kc_chunk_nonneg == 4
+    x, sf = _act(n, cin, hw)
+    ho = (hw - 3) // stride + 1
+    # exact per-row sums: 9 taps x (30 * 255 * 511 + 255) (odd per step; 5 steps > 2^24)
+    per_step = SAT * 255 * 511 + 255
+    assert per_step * 4 <= 2**24 < per_step * 5 and per_step % 2 == 1
+    total = 9 * per_step
+    sc = torch.ones(cout, dtype=torch.float64, device=DEV)
+    sh = torch.full((cout,), -float(total), dtype=torch.float64, device=DEV)
+    sh[cout - 1] = -256.0 * 511
+    outs = []
+    cm = torch.empty((n, hw, hw, 64), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(x, True, sf, 9, 3, cm)
+    for cfg in range(0, tq_native.lib().tq_conv2d_mfma_num_configs() + 1):
+        o = torch.full((n, cout, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        tq_native.conv2d_termpair_fused(cm, lay_m.w_codes, cout, 3, 3, (stride, stride),
+                                        (0, 0), (1, 1), ho, ho, out=o, ch_scale=sc, ch_shift=sh,
+                                        config=cfg, kc_steps=lay_m.kc_steps_nonneg,
+                                        kc_chunk=lay_m.kc_chunk_nonneg)
+        outs.append(o.cpu())
+    lay_v = _layer(cin, cout, stride, "valu", monkeypatch)
+    ci = torch.empty((n, hw, hw, 64), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x, True, sf, 9, 3, ci)
+    o = torch.full((n, cout, ho, ho), float("nan"), device=DEV).contiguous(
+        memory_format=torch.channels_last)
+    tq_native.conv2d_termpair_fused(ci, lay_v.w_codes, cout, 3, 3, (stride, stride), (0, 0),
+                                    (1, 1), ho, ho, out=o, ch_scale=sc, ch_shift=sh)
+    ref = o.cpu()
+    # y = acc - expected: exactly 0 everywhere when every partial sum was exact
+    assert torch.equal(ref, torch.zeros_like(ref))
+    for i, got in enumerate(outs):
+        assert torch.equal(got, ref), "config %d" % i
+
+
+@pytest.mark.parametrize("engine", ["mfma", "valu"])
+def test_epilogue_zeroes_code_padding(engine, monkeypatch):
+    """Cout = 12: codes_a has Cp = 16, the epilogue writes channels 12..15 as zero codes even
+    into a buffer prefilled with NaN bits; the consumer then matches the fp64 reference."""
+    import tq_fuse
+    monkeypatch.setenv("TQ_CONV_ENGINE", engine)
+    torch.manual_seed(21)
+    c1 = nn.Conv2d(16, 12, 3, 1, 1, bias=False)
+    c2 = nn.Conv2d(12, 20, 3, 1, 1, bias=True)
+    a = tr_layer.TRConv2dLayer(c1.to(DEV), 9, 3, 9, 4, 6)
+    b = tr_layer.TRConv2dLayer(c2.to(DEV), 9, 3, 9, 4, 6)
+    for lay, sf in ((a, 0.03), (b, 0.05)):
+        lay.input_quant.tracking = False
+        lay.input_quant.sf = sf
+    ca, cb = tq_fuse._Conv(a, None), tq_fuse._Conv(b, None)
+    x = torch.relu(torch.randn(2, 16, 9, 9, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.empty((2, 9, 9, 16), dtype=ca.code_dtype, device=DEV)
+    tq_native.act_encode(x, True, 0.03, 9, 3, codes)
+    mid = torch.empty((2, 9, 9, 16), dtype=cb.code_dtype, device=DEV)
+    mid.view(torch.int16).fill_(0x7E00 if engine == "mfma" else -1)  # NaN fp16 / junk
+    y1 = torch.empty((2, 12, 9, 9), device=DEV).contiguous(memory_format=torch.channels_last)
+    ws = tq_native.conv2d_workspace(2 * 81, 12, DEV)
+    tq_native.conv2d_termpair_fused(codes, a.w_codes, 12, 3, 3, (1, 1), (1, 1), (1, 1), 9, 9,
+                                    out=y1, ch_scale=ca.scale, ch_shift=ca.shift, relu=True,
+                                    codes_a=mid, quant_a=cb.quant, workspace=ws,
+                                    kc_steps=ca.kc_steps, kc_chunk=ca.kc_chunk)
+    assert not mid[..., 12:].view(torch.int16).any()
+    y2 = torch.empty((2, 20, 9, 9), device=DEV).contiguous(memory_format=torch.channels_last)
+    ws2 = tq_native.conv2d_workspace(2 * 81, 20, DEV)
+    tq_native.conv2d_termpair_fused(mid, b.w_codes, 20, 3, 3, (1, 1), (1, 1), (1, 1), 9, 9,
+                                    out=y2, ch_scale=cb.scale, ch_shift=cb.shift,
+                                    workspace=ws2, kc_steps=cb.kc_steps, kc_chunk=cb.kc_chunk)
+    yq = oracle.tr(y1.contiguous().cpu().numpy().reshape(1, -1, 1, 1), 0.05, 9, 1, 3)
+    xq = torch.from_numpy(yq).view(y1.shape).double()
+    wq = b.conv.weight.detach().double().cpu()
+    ref = F.conv2d(xq, wq, b.conv.bias.detach().double().cpu(), 1, 1)
+    mag = F.conv2d(xq.abs(), wq.abs(), None, 1, 1)
+    got = y2.double().cpu()
+    assert bool(torch.isfinite(got).all())
+    assert bool(((got - ref).abs() <= 1e-5 * torch.maximum(ref.abs(), mag) + 1e-30).all())
+    exp_codes = np.rint(yq.reshape(y1.shape) / np.float32(0.05)).astype(np.int64)
+    assert torch.equal(mid[..., :12].cpu().long().permute(0, 3, 1, 2),
+                       torch.from_numpy(exp_codes))

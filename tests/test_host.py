@@ -418,3 +418,36 @@ def test_mfma_flush_nonneg_windows():
         assert gen != -1 or got == -1
         if gen > 0:
             assert got == 0 or got >= gen
+
+
+def test_mfma_flush_chunk_nonneg_brute_force():
+    """mfma_flush_chunk(nonneg=True) against its spec by brute force, in the chunk-major
+    order the input-patch engine walks (each 64-channel chunk, all taps)."""
+    import tq_ops  # noqa: F811
+    g = torch.Generator().manual_seed(9)
+    for trial in range(5):
+        cout, cin, kh = 6, 192, 3
+        codes = torch.randint(-256, 257, (cout, cin, kh, kh), generator=g, dtype=torch.int32)
+        if trial % 2:
+            codes[:, :96] = codes[:, :96].abs()
+        packed, cp = tq_ops.pack_conv_weight(codes, "mfma")
+        db = 9
+        lim = 2.0**24 / 2**db
+        nch, ntaps = cp // 64, kh * kh
+        st = packed.double().view(packed.shape[0], -1, 64)  # [O, tap * nch + c, 64]
+        pos, neg = st.clamp(min=0).sum(-1), (-st).clamp(min=0).sum(-1)
+
+        def ok(n):
+            for c in range(nch):
+                for i in range(ntaps - n + 1):
+                    taps = [(i + t) * nch + c for t in range(n)]
+                    if max(float(pos[:, taps].sum(1).max()), float(neg[:, taps].sum(1).max())) \
+                            > lim:
+                        return False
+            return True
+        best = max([n for n in range(1, ntaps + 1) if ok(n)], default=0)
+        exp = -1 if best == 0 else (0 if best == ntaps else best)
+        assert tq_ops.mfma_flush_chunk(packed, db, cp, ntaps, nonneg=True) == exp
+        gen = tq_ops.mfma_flush_chunk(packed, db, cp, ntaps)
+        if gen > 0:
+            assert exp == 0 or exp >= gen
