@@ -1,45 +1,53 @@
-"""WikiText-2 tokenisation -- the reference's lstm_models/data.py (Dictionary, Corpus)."""
+"""WikiText-2 token ids for evaluate_lstm.py (the reference keeps the PyTorch word-LM
+example's Dictionary/Corpus in lstm_models/data.py:1-48; this is a separate implementation of
+the same contract: one vocabulary over train, valid and test in that order, every line's
+words followed by '<eos>', splits as int64 id tensors).
+
+The reference snapshot lacks train.txt (.MISSING_LARGE_BLOBS), so the 33,278-word vocabulary
+-- and therefore the test-split ids -- cannot be rebuilt offline; evaluate_lstm.py
+--synthetic draws ids from that vocabulary size instead."""
 import os
-from io import open
 
 import torch
 
+SPLITS = ("train", "valid", "test")
 
-class Dictionary(object):
+
+def _words(path):
+    with open(path, "r", encoding="utf8") as f:
+        for line in f:
+            yield from line.split()
+            yield "<eos>"
+
+
+class Vocabulary(object):
+    """word -> id in first-seen order; ``idx2word`` / ``word2idx`` / ``len`` as the example's
+    Dictionary exposes them."""
+
     def __init__(self):
         self.word2idx = {}
-        self.idx2word = []
+
+    @property
+    def idx2word(self):
+        return list(self.word2idx)
 
     def add_word(self, word):
-        if word not in self.word2idx:
-            self.idx2word.append(word)
-            self.word2idx[word] = len(self.idx2word) - 1
-        return self.word2idx[word]
+        return self.word2idx.setdefault(word, len(self.word2idx))
 
     def __len__(self):
-        return len(self.idx2word)
+        return len(self.word2idx)
 
 
 class Corpus(object):
-    """Vocabulary built from train, valid, test in that order (lstm_models/data.py:20-48);
-    the reference snapshot lacks train.txt, so the 33,278-word vocabulary -- and the test
-    token ids -- cannot be rebuilt offline."""
-
     def __init__(self, path):
-        self.dictionary = Dictionary()
-        self.train = self.tokenize(os.path.join(path, 'train.txt'))
-        self.valid = self.tokenize(os.path.join(path, 'valid.txt'))
-        self.test = self.tokenize(os.path.join(path, 'test.txt'))
-
-    def tokenize(self, path):
-        assert os.path.exists(path), path
-        with open(path, 'r', encoding="utf8") as f:
-            for line in f:
-                for word in line.split() + ['<eos>']:
-                    self.dictionary.add_word(word)
-        with open(path, 'r', encoding="utf8") as f:
-            idss = []
-            for line in f:
-                ids = [self.dictionary.word2idx[w] for w in line.split() + ['<eos>']]
-                idss.append(torch.tensor(ids).type(torch.int64))
-        return torch.cat(idss)
+        files = {s: os.path.join(path, s + ".txt") for s in SPLITS}
+        missing = [f for f in files.values() if not os.path.exists(f)]
+        if missing:
+            raise FileNotFoundError("WikiText-2 split(s) missing: %s" % ", ".join(missing))
+        self.dictionary = Vocabulary()
+        for s in SPLITS:  # the vocabulary sees every split before any is encoded
+            for w in _words(files[s]):
+                self.dictionary.add_word(w)
+        ids = self.dictionary.word2idx
+        for s in SPLITS:
+            setattr(self, s, torch.tensor([ids[w] for w in _words(files[s])], dtype=torch.int64))

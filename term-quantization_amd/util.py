@@ -1,5 +1,6 @@
-"""Evaluation helpers -- the reference's util.py (util.py:1-133): ``validate``, ``accuracy``,
-``AverageMeter``, ``ProgressMeter``, ``get_imagenet_validation``; plus a synthetic
+"""Evaluation helpers -- the reference's util.py roles (util.py:1-133): ``validate``,
+``accuracy``, ``get_imagenet_validation`` (its AverageMeter/ProgressMeter printing is folded
+into validate's progress line); plus a synthetic
 ImageNet-shaped loader (no dataset is available offline) and the distributed accuracy
 reduction that replaces nn.DataParallel's gather-to-GPU0."""
 import os
@@ -79,111 +80,54 @@ class SyntheticImageNet(object):
 
 
 def validate(val_loader, model, criterion, args, verbose=True, pct=1.0):
-    """Top-1 evaluation loop (util.py:39-80).  Under torch.distributed the loss and
-    correct-count sums are all-reduced once at the end, so every rank returns the global
-    figures (the reference reads GPU0's DataParallel gather)."""
-    batch_time = AverageMeter('Time', ':6.3f')
-    losses = AverageMeter('Loss', ':.4e')
-    top1 = AverageMeter('Acc@1', ':6.2f')
-    progress = ProgressMeter(len(val_loader), [batch_time, losses, top1], prefix='Test: ')
-
+    """Top-1 evaluation loop over (pct of) the loader (util.py:39-80): returns (mean loss,
+    top-1 %) weighted by batch size.  Under torch.distributed the loss / correct / sample
+    sums are all-reduced once at the end, so every rank returns the global figures (the
+    reference reads GPU0's DataParallel gather)."""
     model.eval()
     eval_samples = round(pct * len(val_loader.dataset.targets))
-    curr_samples = 0
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-
+    seen = 0
+    totals = [0.0, 0.0, 0.0]  # sum of loss * n, sum of top-1 % * n, n (this rank)
+    tick = time.time()
     with torch.no_grad():
-        end = time.time()
         for i, (images, target) in enumerate(val_loader):
             if args.gpu is not None:
                 images = images.cuda(args.gpu, non_blocking=True)
-            curr_samples += len(target) * world
-            if args.gpu is not None:
                 target = target.cuda(args.gpu, non_blocking=True)
-
+            seen += len(target) * world
             output = model(images)
-            loss = criterion(output, target)
-
-            acc1 = accuracy(output, target, topk=1)
-            losses.update(loss.item(), images.size(0))
-            top1.update(acc1, images.size(0))
-
-            batch_time.update(time.time() - end)
-            end = time.time()
-
-            if i % args.print_freq == 0 and verbose:
-                progress.display(i)
-
-            if curr_samples >= eval_samples:
+            n = images.size(0)
+            loss, acc1 = criterion(output, target).item(), accuracy(output, target, topk=1)
+            totals[0] += loss * n
+            totals[1] += acc1 * n
+            totals[2] += n
+            if verbose and i % args.print_freq == 0:  # batch value (running mean)
+                now = time.time()
+                print("Test: [%d/%d]\tTime %.3f\tLoss %.4e (%.4e)\tAcc@1 %.2f (%.2f)" % (
+                    i, len(val_loader), now - tick, loss, totals[0] / totals[2], acc1,
+                    totals[1] / totals[2]))
+                tick = now
+            if seen >= eval_samples:
                 break
-
     if world > 1:
         dev = torch.device('cuda', args.gpu) if args.gpu is not None else torch.device('cpu')
-        t = torch.tensor([losses.sum, top1.sum, float(top1.count)], dtype=torch.float64,
-                         device=dev)
+        t = torch.tensor(totals, dtype=torch.float64, device=dev)
         dist.all_reduce(t)
-        losses.avg = t[0].item() / max(t[2].item(), 1.0)
-        top1.avg = t[1].item() / max(t[2].item(), 1.0)
-
+        totals = t.tolist()
+    loss = totals[0] / max(totals[2], 1.0)
+    top1 = totals[1] / max(totals[2], 1.0)
     if verbose:
-        print(' * Acc@1 {top1.avg:.3f} '.format(top1=top1))
-
-    return losses.avg, top1.avg
-
-
-class AverageMeter(object):
-    """Computes and stores the average and current value"""
-
-    def __init__(self, name, fmt=':f'):
-        self.name = name
-        self.fmt = fmt
-        self.reset()
-
-    def reset(self):
-        self.val = 0
-        self.avg = 0
-        self.sum = 0
-        self.count = 0
-
-    def update(self, val, n=1):
-        self.val = val
-        self.sum += val * n
-        self.count += n
-        self.avg = self.sum / self.count
-
-    def __str__(self):
-        fmtstr = '{name} {val' + self.fmt + '} ({avg' + self.fmt + '})'
-        return fmtstr.format(**self.__dict__)
-
-
-class ProgressMeter(object):
-    def __init__(self, num_batches, meters, prefix=""):
-        self.batch_fmtstr = self._get_batch_fmtstr(num_batches)
-        self.meters = meters
-        self.prefix = prefix
-
-    def display(self, batch):
-        entries = [self.prefix + self.batch_fmtstr.format(batch)]
-        entries += [str(meter) for meter in self.meters]
-        print('\t'.join(entries))
-
-    def _get_batch_fmtstr(self, num_batches):
-        num_digits = len(str(num_batches // 1))
-        fmt = '{:' + str(num_digits) + 'd}'
-        return '[' + fmt + '/' + fmt.format(num_batches) + ']'
+        print(' * Acc@1 %.3f ' % top1)
+    return loss, top1
 
 
 def accuracy(output, target, topk=1):
-    '''Computes the accuracy over the k top predictions'''
+    """Percentage of rows whose target is among the ``topk`` highest outputs (the
+    reference's util.accuracy for one k, util.py:123-133)."""
     with torch.no_grad():
-        batch_size = target.size(0)
-
-        _, pred = output.topk(topk, 1, True, True)
-        pred = pred.t()
-        correct = pred.eq(target.view(1, -1).expand_as(pred))
-
-        correct_k = correct[:topk].reshape(-1).float().sum(0, keepdim=True)
-        return correct_k.mul_(100.0 / batch_size).item()
+        hits = (output.topk(topk, dim=1).indices == target.view(-1, 1)).any(dim=1)
+        return 100.0 * hits.float().mean().item()
 
 
 def allreduce_histograms(model):
