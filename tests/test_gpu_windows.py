@@ -140,3 +140,50 @@ def test_epilogue_zeroes_code_padding(engine, monkeypatch):
     exp_codes = np.rint(yq.reshape(y1.shape) / np.float32(0.05)).astype(np.int64)
     assert torch.equal(mid[..., :12].cpu().long().permute(0, 3, 1, 2),
                        torch.from_numpy(exp_codes))
+
+
+@pytest.mark.parametrize("engine", ["mfma", "valu"])
+@pytest.mark.parametrize("shift", [0.0, 1e-7, -1e-7, 3.3e-6])
+def test_epilogue_codes_at_rounding_midpoints(engine, shift, monkeypatch):
+    """The epilogue's fast path for the next layer's codes (division-free quotient, fract
+    rounding, top-bit peel) against the oracle's true division, on outputs that sit on and
+    around rounding midpoints: a 1x1 conv whose weights are 256 * identity,
+    scale sc, and next sf = 2 * sc * 256 / 256, so y / sf = acc / 512 * 256 / 2 = x_code / 2
+    -- every odd activation code lands on q + 0.5 exactly (before the shift moves it by a
+    few ulps)."""
+    import tq_fuse
+    monkeypatch.setenv("TQ_CONV_ENGINE", engine)
+    c = 64
+    conv = nn.Conv2d(c, c, 1, 1, 0, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(torch.eye(c).view(c, c, 1, 1) * 0.5)
+    lay = tr_layer.TRConv2dLayer(conv.to(DEV), 10, 10, 9, 1, 9)
+    lay.input_quant.tracking = False
+    lay.input_quant.sf = 1.0
+    cv = tq_fuse._Conv(lay, None)
+    sc = 0.0371
+    n, hw = 2, 16
+    # activation codes 0..1023 (10 bits, all terms kept): x = code * sf_x
+    xc = torch.arange(n * c * hw * hw, dtype=torch.float32).remainder(1024).view(n, c, hw, hw)
+    x = xc.to(DEV).contiguous(memory_format=torch.channels_last)
+    codes = torch.empty((n, hw, hw, c), dtype=cv.code_dtype, device=DEV)
+    tq_native.act_encode(x, True, 1.0, 10, 10, codes)
+    ws = tq_native.conv2d_workspace(n * hw * hw, c, DEV)
+    scv = torch.full((c,), sc / 256.0, dtype=torch.float64, device=DEV)  # acc = 256 * code
+    shv = torch.full((c,), shift, dtype=torch.float64, device=DEV)
+    sf_next = 2.0 * sc
+    y = torch.empty((n, c, hw, hw), device=DEV).contiguous(memory_format=torch.channels_last)
+    ca = torch.empty((n, hw, hw, c), dtype=cv.code_dtype, device=DEV)
+    tq_native.conv2d_termpair_fused(codes, lay.w_codes, c, 1, 1, (1, 1), (0, 0), (1, 1), hw, hw,
+                                    out=y, ch_scale=scv, ch_shift=shv, relu=True, codes_a=ca,
+                                    quant_a=(sf_next, 9, 3), workspace=ws,
+                                    kc_steps=cv.kc_steps, kc_chunk=cv.kc_chunk)
+    yn = y.contiguous().cpu().numpy()
+    exp = np.rint(oracle.tr(yn.reshape(1, -1, 1, 1), sf_next, 9, 1, 3).reshape(yn.shape) /
+                  np.float32(sf_next)).astype(np.int64)
+    got = ca.cpu().long().permute(0, 3, 1, 2).numpy()
+    np.testing.assert_array_equal(got, exp)
+    # the inputs do straddle midpoints: y / sf within 4 ulps of a half-integer for many
+    r = (yn / np.float32(sf_next)).astype(np.float32)
+    near = np.abs(r - np.floor(r) - 0.5) <= 4 * np.spacing(r)
+    assert near.sum() > 1000

@@ -365,30 +365,40 @@ def test_hese_max_terms():
 
 
 def test_relu_fast_path_restatement():
-    """csrc/tq_device.h tr_values_relu4, restated in numpy: the fract-based rounding and the
-    top-bit peel (capped at hese_max_terms) give the oracle's TR value for y >= 0."""
+    """csrc/tq_device.h tr_values_relu4, restated in numpy: the division-free quotient
+    fp32(double(y) * RN64(1/sf)), the fract-based rounding and the top-bit peel (capped at
+    hese_max_terms) give the oracle's TR value for y >= 0 -- including values placed on and a
+    few ulps around every rounding midpoint."""
     rng = np.random.default_rng(0)
     for bw, k in [(9, 3), (9, 0), (9, 1), (9, 12), (8, 8), (11, 4), (4, 2), (14, 5)]:
         maxv = np.float32(2 ** bw - 1)
-        sf = np.float32(0.037)
-        y = np.concatenate([rng.exponential(2.0 ** bw * 0.02, 20000),
-                            (np.arange(0, 2 ** bw + 8) + 0.5) * 0.037,
-                            [0.0, np.inf, 1e30]]).astype(np.float32)
-        r = np.minimum((y.astype(np.float64) * (1.0 / np.float64(sf))).astype(np.float32), maxv)
-        fl = np.floor(r)
-        q = (fl.astype(np.int64) + ((r - fl) >= 0.5)).astype(np.int64)
-        pos, neg = _hese_masks_np(q)
-        m = pos | neg
-        rest = m.copy()
-        for _ in range(min(k, 2 * (bw + 1) // 3)):
-            nz = rest > 0
-            top = np.zeros_like(rest)
-            top[nz] = 1 << np.floor(np.log2(rest[nz])).astype(np.int64)
-            rest = rest & ~top
-        keep = m ^ rest
-        got = (pos & keep) - (neg & keep)
-        exp = oracle.tr(y.reshape(1, -1, 1, 1), float(sf), bw, 1, k).reshape(-1) / sf
-        np.testing.assert_array_equal(got.astype(np.float64), np.round(exp.astype(np.float64)))
+        for sf in (np.float32(0.037), np.float32(1.0), np.float32(3.3e-5)):
+            mids = ((np.arange(0, 2 ** bw + 8) + 0.5) * np.float64(sf)).astype(np.float32)
+            around = np.concatenate([mids] + [np.nextafter(mids, np.float32(np.inf) * d)
+                                              for d in (1, -1)] +
+                                    [np.nextafter(np.nextafter(mids, np.float32(np.inf)),
+                                                  np.float32(np.inf))])
+            y = np.concatenate([rng.exponential(2.0 ** bw * float(sf) * 0.02, 20000), around,
+                                [0.0, np.inf, 1e30]]).astype(np.float32)
+            inv = 1.0 / np.float64(sf)
+            with np.errstate(over="ignore"):
+                t = (y.astype(np.float64) * inv).astype(np.float32)  # quotient_f32
+            r = np.minimum(t, maxv)
+            fl = np.floor(r)
+            q = (fl.astype(np.int64) + ((r - fl) >= 0.5)).astype(np.int64)
+            pos, neg = _hese_masks_np(q)
+            m = pos | neg
+            rest = m.copy()
+            for _ in range(min(k, 2 * (bw + 1) // 3)):
+                nz = rest > 0
+                top = np.zeros_like(rest)
+                top[nz] = 1 << np.floor(np.log2(rest[nz])).astype(np.int64)
+                rest = rest & ~top
+            keep = m ^ rest
+            got = (pos & keep) - (neg & keep)
+            exp = oracle.tr(y.reshape(1, -1, 1, 1), float(sf), bw, 1, k).reshape(-1) / sf
+            np.testing.assert_array_equal(got.astype(np.float64),
+                                          np.round(exp.astype(np.float64)))
 
 
 def test_mfma_flush_nonneg_windows():
