@@ -35,6 +35,7 @@ import util  # noqa: E402
 METRIC = "term-pair MACs/sec + images/sec, ResNet-18 TQ g=8 at 1/2/4/8 MI355X"
 WB, G, K, DB, DT = 9, 8, 12, 9, 3
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+HBM_BYTES_PER_IMAGE = 15026432   # algorithmic bytes of the TR path per image
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes x clock = 78.6e12 lane-op/s
 # v_dot2c_i32_i16 issues at half the VALU rate on gfx950 (4 cycles per wave64; measured
 # 35.8e12 lane-op/s by tools/valu_peak.hip) and does 2 int16 MACs per lane-op:
@@ -51,7 +52,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--cpu-sample", type=int, default=24,
+    ap.add_argument("--cpu-sample", type=int, default=64,
                     help="images in the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--engine", choices=("mfma", "valu"), default="mfma",
@@ -72,8 +73,9 @@ class KernelTimer(object):
     def __init__(self):
         self.events = {}
         self.work = {}
+        self.nbytes = {}
 
-    def __call__(self, name, work, fn):
+    def __call__(self, name, work, fn, nbytes=0):
         s = torch.cuda.current_stream()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
@@ -82,13 +84,15 @@ class KernelTimer(object):
         b.record(s)
         self.events.setdefault(name, []).append((a, b))
         self.work[name] = self.work.get(name, 0) + work
+        self.nbytes[name] = self.nbytes.get(name, 0) + nbytes
         return r
 
     def summary(self):
         out = {}
         for name, evs in self.events.items():
             t = sum(a.elapsed_time(b) for a, b in evs) * 1e-3
-            out[name] = {"launches": len(evs), "seconds": t, "work": self.work[name]}
+            out[name] = {"launches": len(evs), "seconds": t, "work": self.work[name],
+                         "bytes": self.nbytes[name]}
         return out
 
 
@@ -113,14 +117,48 @@ def build_model(dev, batch, seed):
     return model, qmodel, tmacs
 
 
+def host_info():
+    """CPU of this host: model name (/proc/cpuinfo), logical CPUs (nproc) and the threads a
+    baseline may use (OMP_NUM_THREADS: 16 on the GPU box, its CPU share; else nproc)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS") or nproc)
+    return model, nproc, max(1, min(threads, nproc))
+
+
 def cpu_baseline(model_fp, qmodel, nimg):
-    """The oracle (C restatement of the reference kernel, 1 thread) TR-ing every activation,
-    with the reference's dense fp32 torch conv (1 thread) on the fake-quantized tensors --
-    the reference algorithm on the host, timed on a bounded sample."""
+    """The reference algorithm on the host, on all the CPU threads this job may use: the
+    oracle (C restatement of the reference kernel) TR-ing every TR-layer activation, split in
+    chunks over a thread pool (g = 1 is elementwise; ctypes releases the GIL), and the
+    reference's dense fp32 torch conv (torch.set_num_threads) on the fake-quantized tensors;
+    timed on a bounded sample of the bench workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     import copy
     import torch.nn as nn
+    from concurrent.futures import ThreadPoolExecutor
+    cpu_model, nproc, threads = host_info()
+    pool = ThreadPoolExecutor(threads)
+
+    def tr_parallel(x, sf, db, dt):
+        flat = x.contiguous().numpy().reshape(-1)
+        out = np.empty_like(flat)
+        bounds = np.linspace(0, flat.size, 4 * threads + 1).astype(np.int64)
+
+        def run(j):
+            lo, hi = bounds[j], bounds[j + 1]
+            if hi > lo:
+                out[lo:hi] = oracle.tr(flat[lo:hi].reshape(1, -1, 1, 1), sf, db, 1,
+                                       dt).reshape(-1)
+        list(pool.map(run, range(4 * threads)))
+        return torch.from_numpy(out).view(x.shape)
 
     class OracleTRConv(nn.Module):
         def __init__(self, layer):
@@ -130,9 +168,7 @@ def cpu_baseline(model_fp, qmodel, nimg):
             self.db, self.dt = layer.data_bits, layer.data_terms
 
         def forward(self, x):
-            xq = oracle.tr(x.contiguous().numpy().reshape(1, -1, 1, 1), self.sf, self.db, 1,
-                           self.dt)
-            return self.conv(torch.from_numpy(xq).view(x.shape))
+            return self.conv(tr_parallel(x, self.sf, self.db, self.dt))
 
     cpu = copy.deepcopy(model_fp).cpu().float().eval()
     qmods = dict(qmodel.named_modules())
@@ -144,21 +180,23 @@ def cpu_baseline(model_fp, qmodel, nimg):
                 parent = parent._modules[k]
             parent._modules[keys[-1]] = OracleTRConv(qmods[name])
     nthreads = torch.get_num_threads()
-    torch.set_num_threads(1)
+    torch.set_num_threads(threads)
     try:
         x = util.SyntheticImageNet(nimg, nimg, seed=7).batch(0)[0]
         with torch.no_grad():
-            cpu(x[:1])  # warm the allocator
+            cpu(x[:2])  # warm the allocator and the pool
             t0 = time.perf_counter()
             cpu(x)
             dt = time.perf_counter() - t0
     finally:
         torch.set_num_threads(nthreads)
-    return {"value": nimg / dt, "unit": "images/s", "cores": 1, "kind": "port",
+        pool.shutdown()
+    return {"value": nimg / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cpu_model": cpu_model,
             "sample": "%d synthetic 3x224x224 images, ResNet-18 TQ forward: oracle TR "
-                      "(oracle/tr_oracle.c, 1 thread) on every TR-layer activation + torch-CPU "
-                      "fp32 conv (1 thread) on the fake-quantized tensors; weight TR excluded "
-                      "(one-time conversion)" % nimg,
+                      "(oracle/tr_oracle.c) on every TR-layer activation split over %d threads + "
+                      "torch-CPU fp32 conv (%d threads) on the fake-quantized tensors; weight TR "
+                      "excluded (one-time conversion)" % (nimg, threads, threads),
             "tr_op": cpu_tr_op_baseline(oracle)}
 
 
@@ -166,9 +204,10 @@ def cpu_tr_op_baseline(oracle, n=1 << 24):
     """SURVEY 8(d) CPU baseline (iii): the TR op alone (D1: relu(N(0,1)) activations,
     sf=0.05, db=9, dt=3, g=1) by the C oracle on 1 thread and on T host threads (chunks of the
     flat tensor; elements are independent at g=1 and ctypes releases the GIL), elements/s.
-    T = OMP_NUM_THREADS (16 on the GPU box: its CPU share), else the visible core count."""
+    T = OMP_NUM_THREADS (16 on the GPU box: its CPU share), else the visible core count.
+    Beside it, the product's own host TR op (libtq_host.so, OpenMP, T threads)."""
     from concurrent.futures import ThreadPoolExecutor
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    _, _, threads = host_info()
     x = np.maximum(np.random.default_rng(0).standard_normal(n, dtype=np.float32), 0)
 
     def run(chunk):
@@ -184,10 +223,27 @@ def cpu_tr_op_baseline(oracle, n=1 << 24):
         t0 = time.perf_counter()
         list(ex.map(run, chunks))
         tn = time.perf_counter() - t0
+    host = None
+    try:
+        import tq_native
+        xt = torch.from_numpy(x).view(1, -1, 1, 1)
+        out = torch.empty_like(xt)
+        nt = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        try:
+            tq_native.tr_into_host(xt, out, 0.05, DB, 1, DT)  # warm
+            t0 = time.perf_counter()
+            tq_native.tr_into_host(xt, out, 0.05, DB, 1, DT)
+            host = n / (time.perf_counter() - t0)
+        finally:
+            torch.set_num_threads(nt)
+    except Exception:  # noqa: BLE001 -- the host library is optional here
+        host = None
     return {"elements_per_s_1thread": small.size / t1, "elements_per_s": n / tn,
             "threads": threads, "kind": "port",
             "sample": "%d relu(N(0,1)) fp32 elements, TR g=1 (sf=0.05, db=9, dt=3), "
-                      "oracle/tr_oracle.c" % n}
+                      "oracle/tr_oracle.c" % n,
+            "product_host_tr_elements_per_s": host}
 
 
 def main():
@@ -321,12 +377,22 @@ def main():
                 "unit": "TMAC/s (int16 term-sum products)",
                 "frac": conv_work / conv_t / DOT2_PEAK,
             }
+        conv_bytes = conv["bytes"] / conv["launches"]
         roof.update({
             "traffic": traffic,
             "algorithmic_macs_per_launch": conv_work,
+            # the tensors a conv launch reads/writes once (codes in, weight codes, fp32
+            # residual / output, next layers' codes), beside the PMC-measured traffic
+            "algorithmic_bytes_per_launch": conv_bytes,
+            "achieved_gbs": conv_bytes / conv_t / 1e9,
             "avg_launch_us": conv_t * 1e6,
             "launches": conv["launches"],
             "share_of_step": conv["seconds"] / elapsed,
+            # the north star's HBM roofline of the whole path: 15,026,432
+            # algorithmic bytes per image (fp32 TR-layer inputs + outputs + weights/256) at
+            # the measured images/s against the 8 TB/s HBM peak
+            "hbm_bytes_per_image": HBM_BYTES_PER_IMAGE,
+            "hbm_frac": HBM_BYTES_PER_IMAGE * ips / (HBM_PEAK_GBS * 1e9),
         })
         if enc_name == "stem_conv_pool":
             # the fused stem: near-fp32 conv on split-fp16 MFMAs + BN/ReLU/pool + codes;
@@ -339,14 +405,16 @@ def main():
                           "on split-fp16 v_mfma_f32_16x16x32_f16 + BN/ReLU/max-pool + first "
                           "activation TR -> fp16 codes)",
                 "bound": "mfma",
-                "achieved": 2 * enc_bytes / enc_t / 1e12,
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s (fp32-equivalent)",
-                "frac": 2 * enc_bytes / enc_t / 1e12 / FP32_PEAK_TFLOPS,
+                # what the matrix cores execute: 3 fp16 split products per fp32 MAC, against
+                # the dense fp16 MFMA peak
+                "achieved": 3 * 2 * enc_bytes / enc_t / 1e12,
+                "peak": MFMA_F16_PEAK_TFLOPS,
+                "unit": "TFLOP/s (fp16 MFMA, 3 split products per fp32 MAC)",
+                "frac": 3 * 2 * enc_bytes / enc_t / 1e12 / MFMA_F16_PEAK_TFLOPS,
                 "hbm_gbs": stem_bytes / enc_t / 1e9,
-                # what the matrix cores execute: 3 fp16 split products per fp32 MAC
-                "mfma_f16_tflops": 3 * 2 * enc_bytes / enc_t / 1e12,
-                "mfma_f16_frac": 3 * 2 * enc_bytes / enc_t / 1e12 / MFMA_F16_PEAK_TFLOPS,
+                # secondary: the reference's fp32 conv MACs priced against the fp32 peak
+                "fp32_equiv_tflops": 2 * enc_bytes / enc_t / 1e12,
+                "fp32_equiv_frac": 2 * enc_bytes / enc_t / 1e12 / FP32_PEAK_TFLOPS,
                 "traffic": enc_traffic,
                 "algorithmic_macs_per_launch": enc_bytes,
                 "avg_launch_us": enc_t * 1e6,

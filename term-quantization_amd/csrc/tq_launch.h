@@ -114,5 +114,9 @@ hipError_t launch_conv2d_patch(const ConvArgs& a, int mb, hipStream_t stream);
 // or 2 (128 x 128 tiles).
 bool conv_direct_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream);
+// MFMA row-strip engine (tr_conv_strip.hip): 3x3 stride-1 pad-1 convs with 64 -> 64 channels,
+// W % 8 == 0, W <= 56, kc_steps == 0, NHWC out (ResNet-18 layer 1).
+bool conv_strip_eligible(const ConvArgs& a, int out_nhwc);
+hipError_t launch_conv2d_strip(const ConvArgs& a, hipStream_t stream);
 
 }  // namespace tq

@@ -463,7 +463,8 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // gather (Cp % 64 == 0 and KH*KW <= 64; else 1/2), 7-8 input patch (tr_conv_patch.hip:
 // stride 1, KH*KW >= 2, NHWC out; else the gather default).
 // 9-10 direct (tr_conv_direct.hip: Cp % 64 == 0, NHWC out; 128 x 128 / 64 x 128 tiles).
-int conv_mfma_num_configs() { return 10; }
+// 11 row strip (tr_conv_strip.hip: 3x3/1, 64 -> 64 channels, W <= 56; else the default).
+int conv_mfma_num_configs() { return 11; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
@@ -478,6 +479,11 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   a.ab = ab ? atoi(ab) : 0;
   static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 MB
   if (cfg < 0 && dir && atoi(dir) > 0) cfg = atoi(dir) == 1 ? 9 : 8;
+  static const char* strip = getenv("TQ_STRIP");  // A/B override (tools only): 0 off
+  if (cfg == 10 || (cfg < 0 && !(strip && atoi(strip) == 0))) {
+    if (conv_strip_eligible(a, out_nhwc)) return launch_conv2d_strip(a, stream);
+    if (cfg == 10) cfg = -1;
+  }
   // measured (tools/layer_times.py, ResNet-18 batch 256): the direct engine wins where the
   // fused epilogue dominates -- Cout <= 128 (layer1/2) and 1x1 convs
   if (cfg < 0 && !(dir && atoi(dir) == 0) && conv_direct_eligible(a, out_nhwc) &&

@@ -92,6 +92,10 @@ class _Conv(object):
                 else residual.contiguous(memory_format=torch.channels_last)
         cin = self.layer.conv.in_channels
         ws = tq_native.conv2d_workspace(n * ho * wo, self.cout, dev)
+        # algorithmic HBM bytes: each tensor the launch reads or writes, once
+        nbytes = codes.numel() * codes.element_size() + \
+            self.layer.w_codes.numel() * self.layer.w_codes.element_size() + \
+            sum(t.numel() * t.element_size() for t in (out, res, ca, cb) if t is not None)
         tq_ops._launch(
             "conv2d_termpair", n * ho * wo * self.cout * cin * self.kh * self.kw,
             lambda: tq_native.conv2d_termpair_fused(
@@ -100,7 +104,7 @@ class _Conv(object):
                 ch_shift=self.shift, residual=res, relu=relu, codes_a=ca,
                 quant_a=next_a.quant if next_a else None, codes_b=cb,
                 quant_b=next_b.quant if next_b else None, workspace=ws,
-                kc_steps=self.kc_steps, kc_chunk=self.kc_chunk))
+                kc_steps=self.kc_steps, kc_chunk=self.kc_chunk), nbytes)
         return out, ca, cb
 
 

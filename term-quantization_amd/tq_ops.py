@@ -39,14 +39,15 @@ _kernel_hook = None
 
 
 def set_kernel_hook(hook):
-    """Install ``hook(name, work, launch_fn)`` around the term-pair path's kernel launches
-    (bench.py times them with HIP events on the launch stream); None removes it."""
+    """Install ``hook(name, work, launch_fn, nbytes)`` around the term-pair path's kernel
+    launches (bench.py times them with HIP events on the launch stream; ``nbytes`` = the
+    launch's algorithmic HBM bytes where the caller states them, else 0); None removes it."""
     global _kernel_hook
     _kernel_hook = hook
 
 
-def _launch(name, work, fn):
-    return fn() if _kernel_hook is None else _kernel_hook(name, work, fn)
+def _launch(name, work, fn, nbytes=0):
+    return fn() if _kernel_hook is None else _kernel_hook(name, work, fn, nbytes)
 
 
 def _check_input(input):

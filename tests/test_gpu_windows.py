@@ -187,3 +187,71 @@ def test_epilogue_codes_at_rounding_midpoints(engine, shift, monkeypatch):
     r = (yn / np.float32(sf_next)).astype(np.float32)
     near = np.abs(r - np.floor(r) - 0.5) <= 4 * np.spacing(r)
     assert near.sum() > 1000
+
+
+@pytest.mark.parametrize("shape", [(3, 56, 56), (5, 13, 24), (37, 56, 56), (2, 9, 8)])
+@pytest.mark.parametrize("mode", ["conv1", "conv2", "plain"])
+def test_strip_engine_bit_identical(shape, mode, monkeypatch):
+    """The row-strip engine (tr_conv_strip.hip, config 11: layer-1 shapes, 64 -> 64, 3x3/1)
+    against the direct engine (config 10): the same exact integer sums and epilogue, so every
+    fp32 output and code must be bit-identical -- with a partial last strip (H % 4 != 0),
+    narrow images, batches that leave teams without tiles, NaN-prefilled outputs, and the
+    epilogue shapes the executor uses (codes only / plain fp32; residual + fp32 + two code
+    targets is not strip-eligible and must come back from the fallback unchanged)."""
+    monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
+    n, h, w = shape
+    torch.manual_seed(n * 100 + h)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False)
+    nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+    lay = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 9, 8, 12)
+    assert lay.engine == "mfma" and lay.kc_steps_nonneg == 0 and lay.kc_steps == 0
+    x = torch.relu(torch.randn(n, 64, h, w, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.empty((n, h, w, 64), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    sc = torch.rand(64, dtype=torch.float64, device=DEV) * 1e-4
+    sh = torch.randn(64, dtype=torch.float64, device=DEV) * 0.1
+    res = torch.randn(n, 64, h, w, device=DEV).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for cfg in (10, 11):
+        o = torch.full((n, 64, h, w), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.full((n, h, w, 64), float("nan"), dtype=torch.float16, device=DEV)
+        cb = torch.full((n, h, w, 64), float("nan"), dtype=torch.float16, device=DEV)
+        if mode == "plain":  # fp32 output only, no ReLU, no codes
+            tq_native.conv2d_termpair_fused(codes, lay.w_codes, 64, 3, 3, (1, 1), (1, 1),
+                                            (1, 1), h, w, out=o, ch_scale=sc, ch_shift=sh,
+                                            config=cfg, kc_steps=lay.kc_steps)
+        else:
+            tq_native.conv2d_termpair_fused(
+                codes, lay.w_codes, 64, 3, 3, (1, 1), (1, 1), (1, 1), h, w,
+                out=o if mode == "conv2" else None, ch_scale=sc, ch_shift=sh,
+                residual=res if mode == "conv2" else None, relu=True, codes_a=ca,
+                quant_a=(0.05, 9, 3), codes_b=cb if mode == "conv2" else None,
+                quant_b=(0.031, 9, 3) if mode == "conv2" else None, config=cfg,
+                kc_steps=lay.kc_steps_nonneg)
+        outs.append((o.cpu(), ca.cpu(), cb.cpu()))
+    (o0, a0, b0), (o1, a1, b1) = outs
+    if mode != "conv1":
+        assert not torch.isnan(o0).any()
+        _same(o0.permute(0, 2, 3, 1), o1.permute(0, 2, 3, 1), "out")
+    if mode != "plain":
+        _same(a0.view(torch.int16), a1.view(torch.int16), "codes_a")
+        if mode == "conv2":
+            _same(b0.view(torch.int16), b1.view(torch.int16), "codes_b")
+
+
+def _same(ref, got, what):
+    """Bit equality of two NHWC tensors; on failure name where they differ (image, row,
+    column, channel ranges) and whether the strip side holds zeros or NaN prefill."""
+    if torch.equal(ref.view(torch.int32) if ref.dtype == torch.float32 else ref,
+                   got.view(torch.int32) if got.dtype == torch.float32 else got):
+        return
+    bad = (ref != got) & ~(torch.isnan(ref.float()) & torch.isnan(got.float()))
+    idx = bad.nonzero()
+    lo, hi = idx.min(0).values.tolist(), idx.max(0).values.tolist()
+    g = got[bad]
+    raise AssertionError("%s: %d mismatches, n/h/w/c from %s to %s, first %s; strip side "
+                         "zero %d, nan %d" % (what, int(bad.sum()), lo, hi, idx[:4].tolist(),
+                                              int((g == 0).sum()),
+                                              int(torch.isnan(g.float()).sum())))

@@ -34,7 +34,7 @@ def main():
         memory_format=torch.channels_last)
     seq = []
 
-    def hook(name, work, fn):
+    def hook(name, work, fn, nbytes=0):
         s = torch.cuda.current_stream()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
