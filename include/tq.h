@@ -147,6 +147,23 @@ typedef struct tq_conv_epilogue {
   /* code formats (TQ_CODES_*) of codes_a / codes_b: the format of the consuming kernel */
   int32_t fmt_a;
   int32_t fmt_b;
+  /* Fused downsample (tq_conv2d_termpair_f16 only; NULL ds_codes = none): the identity of a
+   * ResNet transition block computed as a second accumulation phase of this launch,
+   *   identity[p][c] = fp32(acc2 * ds_scale[c] + ds_shift[c])
+   * with acc2 the exact term-pair sum of the 1x1, stride ds_stride, pad 0 conv of ds_codes
+   * [n][ds_h][ds_w][ds_cp] (fp16 codes) with ds_w_codes [cout_pad][ds_cp] -- what the
+   * downsample conv with this epilogue would store -- added where `residual` would be
+   * (residual must be NULL; (ds_h - 1) / ds_stride + 1 == ho, likewise w).  ds_cp % 64 == 0,
+   * and every window of the whole ds_cp K range must satisfy the kc_steps bound (no flush).
+   * Replaces the downsample launch and its fp32 identity round trip through HBM. */
+  const uint16_t *ds_codes;
+  int64_t ds_h;
+  int64_t ds_w;
+  int64_t ds_cp;
+  int64_t ds_stride;
+  const uint16_t *ds_w_codes;
+  const double *ds_scale;
+  const double *ds_shift;
 } tq_conv_epilogue;
 
 /* Scratch bytes that let tq_conv2d_termpair_fused use any K-split schedule for an output of
@@ -217,6 +234,25 @@ int tq_dwconv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t
                          float *out, int64_t ho, int64_t wo, int32_t out_nhwc, void *stream);
 
 /*
+ * Term-pair Conv2d (groups = 1) with int32 weight codes, for weight bit widths whose term
+ * sums leave int16 (the (16, 1, 16) squeeze-excite convs of EfficientNet-b0,
+ * cnn_models/__init__.py:57-58; their `self.conv(xq)` at tr_layer.py:124-126):
+ *   out = fp32(acc * scale + bias[c]),  acc = exact int64 sum over (kh, kw, c) of
+ *   act_codes * w_codes.
+ *   act_codes  [n][h][w][cp] int16 (tq_act_encode), cp % 8 == 0, 16-byte aligned
+ *   w_codes    [cout][kp] int32, kp = kh * kw * cp, k = (i*kw + j)*cp + c, 16-byte aligned
+ *   out        [n][cout][ho][wo] (out_nhwc = 0) or [n][ho][wo][cout] (out_nhwc = 1)
+ * Every product must fit int32: |act_code| <= 2^14 and |w_code| <= 2^16 (bitwidths <= 14 /
+ * 16); the int64 sum is exact.
+ */
+int tq_conv2d_termpair_wide(const int16_t *act_codes, int64_t n, int64_t h, int64_t w,
+                            int64_t cp, const int32_t *w_codes, int64_t cout, int64_t kh,
+                            int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
+                            int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                            double scale, const float *bias, float *out, int64_t ho, int64_t wo,
+                            int32_t out_nhwc, void *stream);
+
+/*
  * Stem tail of a TQ ResNet in one pass (the stem conv itself stays fp32, as in the
  * reference): out = relu(maxpool_{k,s,pad}(x * scale[c] + shift[c])) with an eval-mode
  * BatchNorm as (scale, shift), plus the consuming TR layers' activation codes
@@ -267,6 +303,21 @@ int tq_stem_conv_pool_encode(const float *x, int64_t n, int64_t h, int64_t w,
 int tq_mse_profile(const float *x, const float *hist, int64_t nbins, const float *sfs,
                    int64_t nsf, int32_t bitwidth, int32_t num_keep_terms, double *errs,
                    void *stream);
+
+/*
+ * Tracking histogram of the activation calibration, replacing
+ *   self.hist_bins += torch.histc(x, self.num_bins, self.minv, self.maxv)
+ * of LinearQuantize.forward (tr_layer.py:91-94):
+ *   hist[b] += fp32(#{i < numel : x[i] in bin b})          for b < nbins
+ * with torch.histc's GPU bin rule: x outside [minv, maxv] or NaN is skipped, otherwise
+ * b = int(fp32(fp32(x - minv) * nbins) / (maxv - minv)) (fp32 operations), and b == nbins
+ * goes to the last bin.  Counts are exact (torch.histc's fp32 atomic counts stop at 2^24 per
+ * bin).  `x` is any dense fp32 buffer (16-byte aligned); `counts` is uint64 scratch [nbins]
+ * that must be zero on entry and is zero again when the call's work completes.
+ * Domain: 1 <= nbins <= 2^24, minv < maxv.
+ */
+int tq_histc_f32(const float *x, int64_t numel, int64_t nbins, float minv, float maxv,
+                 uint64_t *counts, float *hist, void *stream);
 
 #ifdef __cplusplus
 }

@@ -120,6 +120,22 @@ def mse_profile(hist, minv, maxv, bit_width, terms):
     return sfs[int(np.argmin(np.asarray(errs)))], np.asarray(errs)
 
 
+def histc(x, nbins, minv, maxv):
+    """torch.histc(x, nbins, minv, maxv) as the reference's tracking step calls it
+    (tr_layer.py:91-94), restated in numpy float32 arithmetic: elements outside [minv, maxv]
+    and NaN are skipped, bin = trunc(fp32(fp32(x - minv) * nbins) / (maxv - minv)), bin ==
+    nbins goes to the last bin.  Exact int64 counts.  Pinned against torch.histc itself
+    (CPU in tests/test_oracle.py, GPU in tests/test_gpu_calib.py)."""
+    x = np.asarray(x, dtype=np.float32).reshape(-1)
+    lo, hi = np.float32(minv), np.float32(maxv)
+    x = x[(x >= lo) & (x <= hi)]
+    with np.errstate(over="ignore", invalid="ignore"):
+        b = ((x - lo) * np.float32(nbins)) / np.float32(hi - lo)
+    b = np.trunc(b).astype(np.int64)
+    b[b == nbins] = nbins - 1
+    return np.bincount(b, minlength=nbins).astype(np.int64)
+
+
 def term_pair_macs_conv(out_numel, in_channels, groups, kh, kw, num_terms, weight_bits,
                         group_size, data_terms, data_bits):
     """profile_model.tr_conv2d_ops (profile_model.py:8-26) before the int() truncation."""

@@ -239,6 +239,32 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
   if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: workspace must be 16-byte aligned");
+  if (epi->ds_codes) {
+    if (epi->residual)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: a fused downsample replaces the residual");
+    if (epi->ds_w_codes == nullptr || epi->ds_scale == nullptr || epi->ds_shift == nullptr)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: fused downsample needs weights and coefficients");
+    if (epi->ds_cp < 64 || epi->ds_cp % 64 != 0 || epi->ds_stride < 1 || epi->ds_h < 1 ||
+        epi->ds_w < 1)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad fused downsample shape");
+    if ((epi->ds_h - 1) / epi->ds_stride + 1 != a->Ho ||
+        (epi->ds_w - 1) / epi->ds_stride + 1 != a->Wo)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: fused downsample output size mismatch");
+    if ((uintptr_t)epi->ds_codes % 16 || (uintptr_t)epi->ds_w_codes % 16)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: fused downsample codes must be 16-byte aligned");
+    if ((int64_t)a->N * epi->ds_h * epi->ds_w * epi->ds_cp >= (int64_t)1 << 40)
+      return fail(TQ_ERR_UNSUPPORTED, "conv2d: fused downsample input too large");
+    if (epi->split_k > 1 || epi->split_k < 0)
+      return fail(TQ_ERR_UNSUPPORTED, "conv2d: a fused downsample runs data-parallel only");
+    a->ds_x = reinterpret_cast<const int16_t*>(epi->ds_codes);
+    a->ds_w = reinterpret_cast<const int16_t*>(epi->ds_w_codes);
+    a->ds_scale = epi->ds_scale;
+    a->ds_shift = epi->ds_shift;
+    a->ds_H = (int)epi->ds_h;
+    a->ds_W = (int)epi->ds_w;
+    a->ds_Cp = (int)epi->ds_cp;
+    a->ds_s = (int)epi->ds_stride;
+  }
   a->config = epi->config;
   a->splits = epi->split_k;
   a->ws = epi->workspace;
@@ -274,6 +300,8 @@ int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int
                        pad_h, pad_w, dil_h, dil_w, scale, bias, out, ho, wo, &a);
   if (rc != TQ_OK) return rc;
   if (epi == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: epilogue is null");
+  if (epi->ds_codes)
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d: a fused downsample needs the fp16 (MFMA) entry");
   rc = apply_epilogue(epi, cout, out, tq::conv_num_configs(), &a);
   if (rc != TQ_OK) return rc;
   return hip_status(tq::launch_conv2d_tp(a, 1, (hipStream_t)stream), "conv2d launch");
@@ -308,6 +336,8 @@ int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int6
       return fail(TQ_ERR_UNSUPPORTED, "conv2d_f16: split_k must be 0, 1 or -1");
     rc = apply_epilogue(epi, cout, out, tq::conv_mfma_num_configs(), &a);
     if (rc != TQ_OK) return rc;
+    if (a.ds_x && (a.Cp % 64 != 0 || kh * kw > 64))
+      return fail(TQ_ERR_UNSUPPORTED, "conv2d_f16: a fused downsample needs cp %% 64 == 0");
   }
   return hip_status(tq::launch_conv2d_mfma(a, out_nhwc, (hipStream_t)stream),
                     "conv2d_f16 launch");
@@ -473,6 +503,75 @@ int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float
   return hip_status(tq::launch_mse_profile(x, hist, nbins, sfs, nsf, bitwidth, kk, errs,
                                            (hipStream_t)stream),
                     "mse_profile launch");
+}
+
+int tq_conv2d_termpair_wide(const int16_t* act_codes, int64_t n, int64_t h, int64_t w,
+                            int64_t cp, const int32_t* w_codes, int64_t cout, int64_t kh,
+                            int64_t kw, int64_t kp, int64_t stride_h, int64_t stride_w,
+                            int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                            double scale, const float* bias, float* out, int64_t ho, int64_t wo,
+                            int32_t out_nhwc, void* stream) {
+  if (n < 0 || h < 1 || w < 1 || cout < 1 || kh < 1 || kw < 1 || ho < 1 || wo < 1)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: bad shape");
+  if (cp < 8 || cp % 8 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: cp must be a positive multiple of 8");
+  if (kp != kh * kw * cp)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: kp must be kh * kw * cp");
+  if (stride_h < 1 || stride_w < 1 || dil_h < 1 || dil_w < 1 || pad_h < 0 || pad_w < 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: bad stride/padding/dilation");
+  if ((h + 2 * pad_h - dil_h * (kh - 1) - 1) / stride_h + 1 != ho ||
+      (w + 2 * pad_w - dil_w * (kw - 1) - 1) / stride_w + 1 != wo)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: output size mismatch");
+  if ((uintptr_t)act_codes % 16 || (uintptr_t)w_codes % 16 ||
+      (out_nhwc && (uintptr_t)out % 16))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: buffers must be 16-byte aligned");
+  if (out == nullptr || (n > 0 && (act_codes == nullptr || w_codes == nullptr)))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d_wide: null pointer");
+  if (n * h * w * cp >= (int64_t)1 << 40 || n * ho * wo >= (int64_t)1 << 40 ||
+      cout * kp >= (int64_t)1 << 40 || cout > (1 << 24))
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d_wide: problem too large");
+  tq::WideConvArgs a;
+  a.x = act_codes;
+  a.w = w_codes;
+  a.bias = bias;
+  a.out = out;
+  a.P = n * ho * wo;
+  a.N = (int)n;
+  a.H = (int)h;
+  a.W = (int)w;
+  a.Cp = (int)cp;
+  a.Cout = (int)cout;
+  a.KH = (int)kh;
+  a.KW = (int)kw;
+  a.sh = (int)stride_h;
+  a.sw = (int)stride_w;
+  a.ph = (int)pad_h;
+  a.pw = (int)pad_w;
+  a.dh = (int)dil_h;
+  a.dw = (int)dil_w;
+  a.Ho = (int)ho;
+  a.Wo = (int)wo;
+  a.out_nhwc = out_nhwc ? 1 : 0;
+  a.Kp = kp;
+  a.scale = scale;
+  return hip_status(tq::launch_conv2d_wide(a, (hipStream_t)stream), "conv2d_wide launch");
+}
+
+int tq_histc_f32(const float* x, int64_t numel, int64_t nbins, float minv, float maxv,
+                 uint64_t* counts, float* hist, void* stream) {
+  if (numel < 0 || nbins < 1 || nbins > (1 << 24))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "histc: need numel >= 0 and 1 <= nbins <= 2^24");
+  if (!(minv < maxv))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "histc: need min < max (got %g, %g)", (double)minv,
+                (double)maxv);
+  if (counts == nullptr || hist == nullptr || (numel > 0 && x == nullptr))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "histc: null pointer");
+  if (reinterpret_cast<uintptr_t>(x) % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "histc: x must be 16-byte aligned");
+  return hip_status(tq::launch_histc(x, numel, (int)nbins, minv, maxv,
+                                     reinterpret_cast<unsigned long long*>(counts), hist,
+                                     (hipStream_t)stream),
+                    "histc launch");
 }
 
 }  // extern "C"

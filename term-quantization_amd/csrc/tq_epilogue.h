@@ -53,16 +53,17 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, i
   if (co + 4 == cout && cp > cout) *reinterpret_cast<int2*>(codes + p * cp + co + 4) = make_int2(0, 0);
 }
 
-// emit4_nhwc with the residual already loaded (rv = residual[p][co..co+3], or zeros when
-// there is none): the epilogue issues every residual load of a tile before its first store,
-// so the loads' latency is paid once, not once per output quad.  Cout % 4 == 0.
+// emit4_nhwc with the residual already loaded (rv = residual[p][co..co+3], or the fused
+// downsample's identity, or zeros when there is neither): the epilogue issues every residual
+// load of a tile before its first store, so the loads' latency is paid once, not once per
+// output quad.  Cout % 4 == 0.
 __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int co,
                                                const int acc[4], const double sc[4],
                                                const double sh[4], const float4 rv) {
   float y[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
-  if (a.residual) {
+  if (a.residual || a.ds_x) {
     y[0] += rv.x;
     y[1] += rv.y;
     y[2] += rv.z;

@@ -50,6 +50,16 @@ struct ConvArgs {
   // Execution choices: config 0 = heuristic, 1..conv_num_configs() = a fixed tile config;
   // splits: 1 data-parallel, > 1 K-split with int32 atomics into ws ([P][Cout]), -1
   // stream-K (ws holds two BM x BN int32 slabs per resident block); NHWC output only.
+  // Fused downsample (second accumulation phase; direct engine): the identity of a ResNet
+  // transition block, fp32(acc2 * ds_scale[c] + ds_shift[c]) with acc2 the exact term-pair
+  // sum of the 1x1 stride-ds_s pad-0 conv of ds_x [N][ds_H][ds_W][ds_Cp] with weight codes
+  // ds_w [Cout_pad][ds_Cp], is added where `residual` would be (which must then be null).
+  // The host guarantees acc2's fp32 partial sums need no flush (one window over ds_Cp).
+  const int16_t* ds_x;
+  const int16_t* ds_w;
+  const double* ds_scale;
+  const double* ds_shift;
+  int ds_H, ds_W, ds_Cp, ds_s;
   int ab;  // timing-only A/B switches (TQ_AB, tools only; 0 in the product)
   int config, splits;
   int* ws;
@@ -66,6 +76,19 @@ struct DwConvArgs {
 };
 
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream);
+
+struct WideConvArgs {
+  const int16_t* x;     // activation codes [N][H][W][Cp] (int16), Cp % 8 == 0
+  const int32_t* w;     // weight codes [Cout][Kp] (int32), k = (kh * KW + kw) * Cp + c
+  const float* bias;    // [Cout] or nullptr
+  float* out;           // [N][Ho][Wo][Cout] (out_nhwc) or [N][Cout][Ho][Wo]
+  int64_t P;            // N * Ho * Wo
+  int N, H, W, Cp, Cout, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo, out_nhwc;
+  int64_t Kp;
+  double scale;
+};
+
+hipError_t launch_conv2d_wide(const WideConvArgs& a, hipStream_t stream);
 
 struct PoolArgs {
   const float* x;        // [N][H][W][C] fp32 (channels_last), C % 8 == 0
@@ -103,6 +126,10 @@ int64_t patch_streamk_ws_bytes(int64_t p, int64_t cout);
 hipError_t launch_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                               int64_t nsf, int bitwidth, int k, double* errs, hipStream_t stream);
 hipError_t launch_conv2d_tp(const ConvArgs& a, int out_nhwc, hipStream_t stream);
+// tracking histogram (tq_calib.hip): hist[b] += count of x in bin b (torch.histc bin rule),
+// counts = zeroed uint64 scratch [nbins], left zeroed
+hipError_t launch_histc(const float* x, int64_t n, int nbins, float minv, float maxv,
+                        unsigned long long* counts, float* hist, hipStream_t stream);
 
 // MFMA engine: x, w hold fp16 codes (kCodesF16), Kp % 64 == 0, Cout_pad % 128 == 0.
 hipError_t launch_conv2d_mfma(const ConvArgs& a, int out_nhwc, hipStream_t stream);

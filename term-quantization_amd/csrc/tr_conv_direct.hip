@@ -50,12 +50,18 @@ struct DirCfg {
   static constexpr int LPS = AI + 4;                 // vmem instructions per wave and K-step
 };
 
-template <int MB, bool FLUSH>
+// DS: a second accumulation phase, the fused downsample of a transition block (ConvArgs
+// ds_*): its K-steps (one 1x1 tap, ds_Cp / 64 steps) run through the same pipeline after the
+// main conv's, into fresh fp32 accumulators, while the main conv's sums wait in int32; the
+// epilogue turns them into the identity (what the separate downsample conv would store) and
+// adds it where a residual read from HBM would go.
+template <int MB, bool FLUSH, bool DS>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
   constexpr int NBM = 2 * MB;  // 32-row MFMA blocks per wave
   __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
   __shared__ double coef[C::BM][2];  // epilogue (scale, shift) of the tile's channels
+  __shared__ double coef2[DS ? C::BM : 1][2];  // the fused downsample's (scale, shift)
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = (a.Cout + C::BM - 1) / C::BM;
@@ -83,6 +89,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
   int64_t boff = 0;
   uint64_t tmask = 0;
+  int64_t boff2 = 0;      // DS: the lane's pixel in the downsample's input (1x1, pad 0)
+  uint64_t tmask2 = 0;
   {
     const int64_t p = wn0 + r32;
     if (p < a.P) {
@@ -93,6 +101,11 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
       const int ih0 = oh * a.sh - a.ph;
       const int iw0 = ow * a.sw - a.pw;
       boff = ((img * a.H + ih0) * a.W + iw0) * a.Cp + 8 * hh;
+      if (DS) {
+        boff2 = ((img * a.ds_H + (int64_t)oh * a.ds_s) * a.ds_W + (int64_t)ow * a.ds_s) *
+                    a.ds_Cp + 8 * hh;
+        tmask2 = 1ull;
+      }
       for (int kr = 0; kr < a.KH; ++kr) {
         const int ih = ih0 + kr * a.dh;
         if (ih < 0 || ih >= a.H) continue;
@@ -110,12 +123,18 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     coef[i][0] = a.ch_scale ? (ok ? a.ch_scale[co] : 0.0) : a.scale;
     coef[i][1] = a.ch_scale ? (ok ? a.ch_shift[co] : 0.0)
                             : ((a.bias && ok) ? (double)a.bias[co] : 0.0);
+    if (DS) {
+      coef2[i][0] = ok ? a.ds_scale[co] : 0.0;
+      coef2[i][1] = ok ? a.ds_shift[co] : 0.0;
+    }
   }
 
-  const int nsteps = a.Kp / kKStep;  // = KH * KW * Cp / 64 (Cp % 64 == 0)
+  int nsteps = a.Kp / kKStep;  // = KH * KW * Cp / 64 (Cp % 64 == 0)
   // position of the next K-step to issue, advanced incrementally (no divisions in the loop)
   int i_st = 0, i_tap = 0, i_cb = 0, i_ks = 0;
   int64_t i_toff = 0;  // ((kr * dh) * W + ks * dw) * Cp + cb
+  int cur_cp = a.Cp, cur_kw = a.KW;
+  const uint16_t* __restrict__ xsrc = xg;
   const int64_t row_step = (int64_t)a.dh * a.W * a.Cp;
   const int64_t col_step = (int64_t)a.dw * a.Cp;
   int64_t row_off = 0;
@@ -127,16 +146,16 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
       glds16(arow[i] + (int64_t)i_st * kKStep,
              lds + slot * C::SLOT + (wave * C::AI + i) * 64);
     const bool ok = (tmask >> i_tap) & 1ull;
-    const uint16_t* src = ok ? xg + (boff + i_toff) : zero;
+    const uint16_t* src = ok ? xsrc + (boff + i_toff) : zero;
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[s] = *reinterpret_cast<const u32x4*>(src + 16 * s);
     ++i_st;
     i_cb += kKStep;
     i_toff += kKStep;
-    if (i_cb == a.Cp) {
+    if (i_cb == cur_cp) {
       i_cb = 0;
       ++i_tap;
-      if (++i_ks == a.KW) {
+      if (++i_ks == cur_kw) {
         i_ks = 0;
         row_off += row_step;
         i_toff = row_off;
@@ -147,7 +166,7 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   };
 
   float16v accf[NBM];
-  int acci[FLUSH ? NBM : 1][16];
+  int acci[(FLUSH || DS) ? NBM : 1][16];
 #pragma unroll
   for (int bm = 0; bm < NBM; ++bm) {
 #pragma unroll
@@ -165,7 +184,7 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
         accf[bm][r] = 0.0f;
       }
   };
-  const int kc_steps = a.kc_steps;
+  int kc_steps = a.kc_steps;
   int since_flush = 0;
 
   auto compute = [&](int slot, const u32x4 (&bc)[4]) {
@@ -196,17 +215,47 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     if (s + 2 < nsteps) issue((slot + 2) % kDirSlots, bnext);
     compute(slot, bc);
   };
-  issue(0, b0);
-  if (nsteps > 1) issue(1, b1);
-  int s = 0;
-  for (; s + 2 < nsteps; s += 3) {
-    step(s, 0, b0, b2);
-    step(s + 1, 1, b1, b0);
-    step(s + 2, 2, b2, b1);
-  }
-  if (s < nsteps) step(s, 0, b0, b2);
-  if (s + 1 < nsteps) step(s + 1, 1, b1, b0);
+  auto run = [&]() {
+    issue(0, b0);
+    if (nsteps > 1) issue(1, b1);
+    int s = 0;
+    for (; s + 2 < nsteps; s += 3) {
+      step(s, 0, b0, b2);
+      step(s + 1, 1, b1, b0);
+      step(s + 2, 2, b2, b1);
+    }
+    if (s < nsteps) step(s, 0, b0, b2);
+    if (s + 1 < nsteps) step(s + 1, 1, b1, b0);
+  };
+  run();
   if (FLUSH) flush();
+  if (DS) {
+    // the main conv's exact sums park in acci; the downsample accumulates from zero
+#pragma unroll
+    for (int bm = 0; bm < NBM; ++bm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (!FLUSH) acci[bm][r] = (int)accf[bm][r];
+        accf[bm][r] = 0.0f;
+      }
+    __syncthreads();  // every wave is done reading the ring slots the second phase refills
+#pragma unroll
+    for (int i = 0; i < C::AI; ++i) {
+      const int r = (wave * C::AI + i) * 8 + (lane >> 3);
+      arow[i] = reinterpret_cast<const uint16_t*>(a.ds_w) + (int64_t)(m0 + r) * a.ds_Cp +
+                ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    }
+    nsteps = a.ds_Cp / kKStep;
+    i_st = i_tap = i_cb = i_ks = 0;
+    i_toff = row_off = 0;
+    cur_cp = a.ds_Cp;
+    cur_kw = 1;
+    xsrc = reinterpret_cast<const uint16_t*>(a.ds_x);
+    boff = boff2;
+    tmask = tmask2;
+    kc_steps = 0;  // no flush in the second phase (host-checked window)
+    run();
+  }
 
   // Epilogue.  Lane (slot = lane % SL) finishes channels m0 + 4*slot .. +3 of pixels
   // it*PXI + lane / SL of its wave: each store instruction writes PXI whole pixel rows.
@@ -219,29 +268,56 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   for (int it = 0; it < 32 / PXI; ++it) {
     const int64_t p = wn0 + it * PXI + lane / C::SL;
     res[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (vec && a.residual && co < a.Cout && p < a.P)
+    if (!DS && vec && a.residual && co < a.Cout && p < a.P)
       res[it] = *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co);
   }
   __syncthreads();  // every wave is done with the A ring; coef[] is visible
   u32x4* t = lds + wave * C::TILE;  // [pixel][SL slots of 4 channels], slot ^= pixel & 15
+  // int32 tile (MFMA layout) -> LDS, transposed so a lane reads whole 4-channel quads
+  auto put_tile = [&](bool second) {
 #pragma unroll
-  for (int bm = 0; bm < NBM; ++bm)
+    for (int bm = 0; bm < NBM; ++bm)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int sl = 8 * bm + 2 * q + hh;  // channels 32bm + 8q + 4hh .. +3
-      int v4[4];
+      for (int q = 0; q < 4; ++q) {
+        const int sl = 8 * bm + 2 * q + hh;  // channels 32bm + 8q + 4hh .. +3
+        int v4[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        v4[e] = FLUSH ? acci[bm][4 * q + e] : (int)accf[bm][4 * q + e];
-      u32x4 v;
-      v.x = (uint32_t)v4[0];
-      v.y = (uint32_t)v4[1];
-      v.z = (uint32_t)v4[2];
-      v.w = (uint32_t)v4[3];
-      t[r32 * C::SL + (sl ^ (r32 & 15))] = v;
+        for (int e = 0; e < 4; ++e)
+          v4[e] = (second || !(FLUSH || DS)) ? (int)accf[bm][4 * q + e] : acci[bm][4 * q + e];
+        u32x4 v;
+        v.x = (uint32_t)v4[0];
+        v.y = (uint32_t)v4[1];
+        v.z = (uint32_t)v4[2];
+        v.w = (uint32_t)v4[3];
+        t[r32 * C::SL + (sl ^ (r32 & 15))] = v;
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (DS) {
+    // the identity: fp32(acc2 * ds_scale + ds_shift), as the separate downsample conv stores it
+    put_tile(true);
+    if (co < a.Cout) {
+      double sc2[4], sh2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sc2[i] = coef2[4 * slot + i][0];
+        sh2[i] = coef2[4 * slot + i][1];
+      }
+#pragma unroll
+      for (int it = 0; it < 32 / PXI; ++it) {
+        const int px = it * PXI + lane / C::SL;
+        const u32x4 v = t[px * C::SL + (slot ^ (px & 15))];
+        res[it] = make_float4((float)((double)(int)v.x * sc2[0] + sh2[0]),
+                              (float)((double)(int)v.y * sc2[1] + sh2[1]),
+                              (float)((double)(int)v.z * sc2[2] + sh2[2]),
+                              (float)((double)(int)v.w * sc2[3] + sh2[3]));
+      }
     }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
-  __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // every read of the tile has returned
+    __builtin_amdgcn_wave_barrier();
+  }
+  put_tile(false);
   if (co >= a.Cout) return;
   double sc[4], sh[4];
 #pragma unroll
@@ -263,26 +339,34 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   }
 }
 
-template <int MB, bool FLUSH>
+template <int MB, bool FLUSH, bool DS>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   using C = DirCfg<MB>;
   const int64_t tiles = ((a.P + C::BN - 1) / C::BN) * ((a.Cout + C::BM - 1) / C::BM);
-  conv2d_tp_direct_kernel<MB, FLUSH><<<dim3((unsigned)tiles), kDirThreads, 0, stream>>>(a);
+  conv2d_tp_direct_kernel<MB, FLUSH, DS><<<dim3((unsigned)tiles), kDirThreads, 0, stream>>>(a);
   return hipGetLastError();
+}
+
+template <int MB, bool DS>
+hipError_t launch_direct_mb(const ConvArgs& a, hipStream_t stream) {
+  const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
+  return flush ? launch_direct_cfg<MB, true, DS>(a, stream)
+               : launch_direct_cfg<MB, false, DS>(a, stream);
 }
 
 }  // namespace
 
 bool conv_direct_eligible(const ConvArgs& a, int out_nhwc) {
-  return out_nhwc && a.Cp % kKStep == 0 && a.KH * a.KW <= 64 && a.Kp % kKStep == 0;
+  return out_nhwc && a.Cp % kKStep == 0 && a.KH * a.KW <= 64 && a.Kp % kKStep == 0 &&
+         (a.ds_x == nullptr || a.ds_Cp % kKStep == 0);
 }
 
 // mb: 1 = 64 x 128 tiles, 2 = 128 x 128 tiles.
 hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream) {
-  const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
-  if (mb == 2)
-    return flush ? launch_direct_cfg<2, true>(a, stream) : launch_direct_cfg<2, false>(a, stream);
-  return flush ? launch_direct_cfg<1, true>(a, stream) : launch_direct_cfg<1, false>(a, stream);
+  if (a.ds_x)  // fused downsample: 64-row tiles (the second int32 tile costs registers)
+    return launch_direct_mb<1, true>(a, stream);
+  if (mb == 2) return launch_direct_mb<2, false>(a, stream);
+  return launch_direct_mb<1, false>(a, stream);
 }
 
 }  // namespace tq

@@ -396,7 +396,7 @@ bool conv_strip_eligible(const ConvArgs& a, int out_nhwc) {
          // with a residual the lane-per-channel epilogue (one dword load + store per element)
          // measured slower than the direct engine's 4-channel vectors (218.7 vs 235.8 us,
          // profiles/r02_strip.md): block conv1s only
-         a.residual == nullptr;
+         a.residual == nullptr && a.ds_x == nullptr;
 }
 
 template <bool RES, bool OUT, bool CB>

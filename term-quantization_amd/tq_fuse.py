@@ -16,6 +16,8 @@ the sum rounds to fp32 once, the residual add and ReLU are fp32 as in the module
 each activation code is TR of exactly that fp32 value (tr_layer.py:96-99), so the executor
 matches the module path to fp32 rounding of the BN (DESIGN.md "Fused executor").
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -71,7 +73,28 @@ class _Conv(object):
                 tq_ops.conv_out_size(w, self.kw, self.stride[1], self.padding[1],
                                      self.dilation[1]))
 
-    def __call__(self, codes, out=None, residual=None, relu=False, next_a=None, next_b=None):
+    def fusable_downsample(self, down):
+        """True when ``down`` (a block's 1x1 pad-0 downsample) can run as the second
+        accumulation phase of this conv (tq_conv_epilogue.ds_*): MFMA codes on both, 64-code
+        channel chunks, and a downsample whose fp32 sums need no flush.  Opt-in
+        (TQ_FUSE_DS=1): the phase runs on the direct engine only, and at batch 256 the fused
+        layer-2 conv took as long as conv2 + downsample apart (190.8 vs 158 + 31 us) while the
+        layer-3/4 conv2s lost the input-patch engine (188/198 vs ~121/~102 us + ~15 us;
+        profiles/r02b_summary.json)."""
+        nsteps = down.layer.w_codes.shape[1] // 64
+        return (os.environ.get("TQ_FUSE_DS", "0") == "1" and
+                self.code_dtype == torch.float16 and down.code_dtype == torch.float16 and
+                self.cp_in % 64 == 0 and down.cp_in % 64 == 0 and
+                (down.kh, down.kw) == (1, 1) and tuple(down.padding) == (0, 0) and
+                tuple(down.dilation) == (1, 1) and down.stride[0] == down.stride[1] and
+                down.layer.w_codes.shape[1] == down.cp_in and
+                (down.kc_steps == 0 or down.kc_steps >= nsteps) and
+                down.cout == self.cout)
+
+    def __call__(self, codes, out=None, residual=None, relu=False, next_a=None, next_b=None,
+                 downsample=None):
+        """``downsample`` = (_Conv, its input codes): computed in this launch as a second
+        accumulation phase, its identity added in place of ``residual``."""
         for nxt in (next_a, next_b):
             if nxt is not None and nxt.nonneg and not relu:
                 raise ValueError("a consumer with non-negative windows needs ReLU'd codes")
@@ -96,15 +119,27 @@ class _Conv(object):
         nbytes = codes.numel() * codes.element_size() + \
             self.layer.w_codes.numel() * self.layer.w_codes.element_size() + \
             sum(t.numel() * t.element_size() for t in (out, res, ca, cb) if t is not None)
+        work = n * ho * wo * self.cout * cin * self.kh * self.kw
+        ds = None
+        if downsample is not None:
+            down, dcodes = downsample
+            if res is not None:
+                raise ValueError("a fused downsample replaces the residual")
+            if dcodes.shape[-1] != down.cp_in or not self.fusable_downsample(down):
+                raise ValueError("downsample cannot be fused into this conv")
+            ds = (dcodes, down.layer.w_codes, down.stride[0], down.scale, down.shift)
+            nbytes += dcodes.numel() * dcodes.element_size() + \
+                down.layer.w_codes.numel() * down.layer.w_codes.element_size()
+            work += n * ho * wo * self.cout * down.layer.conv.in_channels
         tq_ops._launch(
-            "conv2d_termpair", n * ho * wo * self.cout * cin * self.kh * self.kw,
+            "conv2d_termpair", work,
             lambda: tq_native.conv2d_termpair_fused(
                 codes, self.layer.w_codes, self.cout, self.kh, self.kw, self.stride,
                 self.padding, self.dilation, ho, wo, out=out, ch_scale=self.scale,
                 ch_shift=self.shift, residual=res, relu=relu, codes_a=ca,
                 quant_a=next_a.quant if next_a else None, codes_b=cb,
                 quant_b=next_b.quant if next_b else None, workspace=ws,
-                kc_steps=self.kc_steps, kc_chunk=self.kc_chunk), nbytes)
+                kc_steps=self.kc_steps, kc_chunk=self.kc_chunk, downsample=ds), nbytes)
         return out, ca, cb
 
 
@@ -247,13 +282,15 @@ class FusedResNet(nn.Module):
             if keep:
                 capture.append({"name": "block%d.conv1" % i, "conv": b.conv1, "codes_in": codes,
                                 "residual": None, "out": y1, "codes_a": mid, "codes_b": None})
-            if b.down is not None:
+            fuse_ds = b.down is not None and b.conv2.fusable_downsample(b.down)
+            if b.down is not None and (not fuse_ds or keep):
+                # (capture runs it separately as well, to record the identity it must equal)
                 identity, _, _ = b.down(codes_down, out=True)
                 if keep:
                     capture.append({"name": "block%d.downsample" % i, "conv": b.down,
                                     "codes_in": codes_down, "residual": None, "out": identity,
                                     "codes_a": None, "codes_b": None})
-            else:
+            elif b.down is None:
                 identity = x
             next_b = nxt.down if nxt is not None and nxt.down is not None else None
             shared = next_b is not None and _same_codes(nxt.conv1, next_b)
@@ -261,9 +298,11 @@ class FusedResNet(nn.Module):
             # (the next identity is the downsample conv's), so only its codes are written
             cin = mid
             x, codes, codes_down = b.conv2(
-                mid, out=True if (next_b is None or keep) else None, residual=identity,
+                mid, out=True if (next_b is None or keep) else None,
+                residual=None if fuse_ds else identity,
                 relu=True, next_a=nxt.conv1 if nxt else None,
-                next_b=None if shared else next_b)
+                next_b=None if shared else next_b,
+                downsample=(b.down, codes_down) if fuse_ds else None)
             if shared:
                 codes_down = codes
             if keep:

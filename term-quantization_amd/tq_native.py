@@ -48,6 +48,10 @@ _SIGNATURES = {
                            _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64, _i32,
                            _vp],
     "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
+    "tq_histc_f32": [_vp, _i64, _i64, _f32, _f32, _vp, _vp, _vp],
+    "tq_conv2d_termpair_wide": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
+                                _i64, _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64,
+                                _i32, _vp],
     "tq_bn_relu_maxpool_encode": [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _i32, _i32,
                                   _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _i32, _vp,
                                   _i64, _f32, _i32, _i32, _i32, _vp],
@@ -64,7 +68,9 @@ class ConvEpilogue(ctypes.Structure):
                 ("codes_b", _vp), ("cp_b", _i64), ("sf_b", _f32), ("bits_b", _i32),
                 ("terms_b", _i32),
                 ("workspace", _vp), ("workspace_bytes", _i64), ("split_k", _i32),
-                ("config", _i32), ("fmt_a", _i32), ("fmt_b", _i32)]
+                ("config", _i32), ("fmt_a", _i32), ("fmt_b", _i32),
+                ("ds_codes", _vp), ("ds_h", _i64), ("ds_w", _i64), ("ds_cp", _i64),
+                ("ds_stride", _i64), ("ds_w_codes", _vp), ("ds_scale", _vp), ("ds_shift", _vp)]
 
 
 _SIGNATURES["tq_conv2d_termpair_fused"] = [
@@ -272,6 +278,21 @@ def conv2d_termpair(codes, w_codes, cout, kh, kw, stride, padding, dilation, sca
     return out
 
 
+def conv2d_termpair_wide(codes, w_codes, cout, kh, kw, stride, padding, dilation, scale, bias,
+                         out, out_nhwc):
+    """Term-pair conv with int32 weight codes (tq_conv2d_termpair_wide): int16 activation
+    codes [n, h, w, cp], w_codes int32 [cout, kh*kw*cp]."""
+    n, h, w, cp = codes.shape
+    ho, wo = out.shape[2], out.shape[3]
+    with torch.cuda.device(codes.device):
+        rc = lib().tq_conv2d_termpair_wide(
+            _ptr(codes), n, h, w, cp, _ptr(w_codes), cout, kh, kw, w_codes.shape[1],
+            stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1],
+            float(scale), _ptr(bias), _ptr(out), ho, wo, int(out_nhwc), _stream(codes))
+    _check(rc)
+    return out
+
+
 def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
     """errs[s] (float64) for each candidate scale factor in sfs (tq_mse_profile)."""
     errs = torch.empty(sfs.numel(), dtype=torch.float64, device=x.device)
@@ -282,15 +303,29 @@ def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
     return errs
 
 
+def histc_accumulate(x, hist, minv, maxv, counts):
+    """hist += torch.histc(x, hist.numel(), minv, maxv) with exact counts (tq_histc_f32).
+    x: dense fp32 CUDA tensor (any memory format); hist: contiguous fp32 [nbins] on x's device;
+    counts: zeroed int64 scratch [nbins] on that device (left zeroed)."""
+    with torch.cuda.device(x.device):
+        rc = lib().tq_histc_f32(_ptr(x), x.numel(), hist.numel(), float(minv), float(maxv),
+                                _ptr(counts), _ptr(hist), _stream(x))
+    _check(rc)
+    return hist
+
+
 def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilation, ho, wo,
                           out=None, ch_scale=None, ch_shift=None, residual=None, relu=False,
                           codes_a=None, quant_a=None, codes_b=None, quant_b=None,
-                          workspace=None, split_k=0, config=0, kc_steps=0, kc_chunk=-1):
+                          workspace=None, split_k=0, config=0, kc_steps=0, kc_chunk=-1,
+                          downsample=None):
     """Term-pair conv with the fused epilogue of tq_conv2d_termpair_fused (channels_last).
     quant_a/_b = (sf, bits, terms) of the layer consuming codes_a/_b, whose dtype (int16 /
     float16) is that layer's code format.  ``workspace`` (int32, >= n*ho*wo*cout elements)
     lets the VALU kernel split the K loop over workgroups.  float16 input codes run the MFMA
-    engine (tq_conv2d_termpair_f16) with flush interval ``kc_steps``."""
+    engine (tq_conv2d_termpair_f16) with flush interval ``kc_steps``.  ``downsample`` =
+    (codes, w_codes, stride, scale, shift): the fused 1x1 downsample phase whose identity
+    replaces ``residual`` (tq_conv_epilogue.ds_*)."""
     n, h, w, cp = codes.shape
     fmt = code_format(codes)
     if code_format(w_codes) != fmt:
@@ -311,6 +346,12 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
     epi.workspace, epi.split_k, epi.config = _ptr(workspace), int(split_k), int(config)
     epi.workspace_bytes = workspace.numel() * workspace.element_size() if workspace is not None \
         else 0
+    if downsample is not None:
+        dcodes, dw, dstride, dscale, dshift = downsample
+        epi.ds_codes, epi.ds_w_codes = _ptr(dcodes), _ptr(dw)
+        epi.ds_h, epi.ds_w, epi.ds_cp = dcodes.shape[1], dcodes.shape[2], dcodes.shape[3]
+        epi.ds_stride = int(dstride)
+        epi.ds_scale, epi.ds_shift = _ptr(dscale), _ptr(dshift)
     with torch.cuda.device(codes.device):
         if fmt == CODES_F16:
             rc = lib().tq_conv2d_termpair_f16(

@@ -100,6 +100,23 @@ def tr_elementwise(x, sf, bitwidth, num_keep_terms):
               num_keep_terms).view(x.shape)
 
 
+def histc_track(x, hist, minv, maxv, counts):
+    """``hist += torch.histc(x, hist.numel(), minv, maxv)`` (tr_layer.py:91-94) for an fp32
+    CUDA tensor on the tracking-histogram kernel (exact integer counts, tq_histc_f32); the
+    memory order of x does not matter.  ``counts``: zeroed int64 scratch [nbins] on x's device.
+    Other tensors (CPU, float64) take torch.histc itself, as the reference does."""
+    if not x.is_cuda or x.dtype != torch.float32:
+        hist += torch.histc(x, hist.numel(), minv, maxv)
+        return hist
+    dense = x.is_contiguous() or (x.dim() == 4 and
+                                  x.is_contiguous(memory_format=torch.channels_last))
+    if not dense:
+        x = x.contiguous()
+    if x.data_ptr() % 16:
+        x = x.clone()
+    return tq_native.histc_accumulate(x, hist, minv, maxv, counts)
+
+
 def tr_encode(w, sf, bitwidth, group_size, num_keep_terms):
     """(TR(w), v) with TR(w) == v * fp32(sf) exactly; v int32 with w's shape."""
     _check_input(w)
@@ -341,7 +358,55 @@ def tr_dwconv2d(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, channe
     _launch("dwconv2d_termpair", n * ho * wo * c * kh * kw,
             lambda: tq_native.dwconv2d_termpair(codes, c, w_packed, kh, kw, stride,
                                                 (top + padding[0], left + padding[1]),
-                                                dilation, scale, bias, out, nhwc))
+                                                dilation, scale, bias, out, nhwc),
+            2 * codes.numel() + 4 * out.numel() + 4 * w_packed.numel())
+    return out
+
+
+MAX_WIDE_WEIGHT_BITS = 16  # tq_conv2d_termpair_wide: |v_x| <= 2^14, |v_w| <= 2^16
+
+
+def pack_wide_weight(codes):
+    """[O, I, KH, KW] int32 term sums -> int32 [O, KH*KW*Cp] with k = (kh*KW + kw)*Cp + c
+    (tq_conv2d_termpair_wide); returns (packed, Cp)."""
+    o, i, kh, kw = codes.shape
+    cp = act_channels(i)
+    t = codes.permute(0, 2, 3, 1)
+    if cp != i:
+        t = torch.nn.functional.pad(t, (0, cp - i))
+    return t.reshape(o, kh * kw * cp).to(torch.int32).contiguous(), cp
+
+
+def tr_conv2d_wide(x, sf_x, data_bits, data_terms, w_packed, cp, sf_w, bias, out_channels,
+                   kernel_size, stride, padding, dilation):
+    """conv2d(TR(x), TR(w)) + bias by exact term-pair accumulation with int32 weight codes
+    (weight bit widths 15-16: EfficientNet-b0's squeeze-excite convs), int64 sums."""
+    if not x.is_cuda:
+        raise RuntimeError("input must be a CUDA tensor")
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("tr_conv2d_wide: expects a 4-D float32 input")
+    n, c, h, w = x.shape
+    if act_channels(c) != cp:
+        raise RuntimeError("tr_conv2d_wide: input has %d channels, weights expect %d" % (c, cp))
+    nhwc = (not x.is_contiguous()) and x.is_contiguous(memory_format=torch.channels_last)
+    if not nhwc and not x.is_contiguous():
+        x = x.contiguous()
+    kh, kw = kernel_size
+    ho = conv_out_size(h, kh, stride[0], padding[0], dilation[0])
+    wo = conv_out_size(w, kw, stride[1], padding[1], dilation[1])
+    codes = torch.empty((n, h, w, cp), dtype=torch.int16, device=x.device)
+    _launch("act_encode", 4 * n * c * h * w + 2 * n * h * w * cp,
+            lambda: tq_native.act_encode(x, nhwc, float(sf_x), int(data_bits), int(data_terms),
+                                         codes))
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    out = torch.empty((n, out_channels, ho, wo), dtype=torch.float32, device=x.device,
+                      memory_format=fmt)
+    scale = float(np.float32(sf_x)) * float(np.float32(sf_w))
+    if bias is not None:
+        bias = bias.detach().to(torch.float32).contiguous()
+    _launch("conv2d_termpair_wide", n * ho * wo * out_channels * c * kh * kw,
+            lambda: tq_native.conv2d_termpair_wide(codes, w_packed, out_channels, kh, kw, stride,
+                                                   padding, dilation, scale, bias, out, nhwc))
     return out
 
 

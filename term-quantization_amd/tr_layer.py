@@ -133,7 +133,17 @@ class LinearQuantize(nn.Module):
 
     def forward(self, x):
         if self.tracking:
-            self.hist_bins += torch.histc(x, self.num_bins, self.minv, self.maxv)
+            # the tracking-histogram kernel for GPU tensors: exact counts (torch.histc's fp32
+            # atomic counts stop at 2^24 per bin), the same bins otherwise
+            if x.is_cuda and self.hist_bins.is_cuda and self.hist_bins.is_contiguous():
+                counts = self.__dict__.get('_hist_counts')
+                if counts is None or counts.device != x.device or \
+                        counts.numel() != self.num_bins:
+                    counts = torch.zeros(self.num_bins, dtype=torch.int64, device=x.device)
+                    self.__dict__['_hist_counts'] = counts
+                tq_ops.histc_track(x, self.hist_bins, self.minv, self.maxv, counts)
+            else:
+                self.hist_bins += torch.histc(x, self.num_bins, self.minv, self.maxv)
             return x
 
         return tq_ops.tr_elementwise(x, self.sf, self.data_bits, self.data_terms)
@@ -185,6 +195,8 @@ class TRConv2dLayer(nn.Module):
                    (fp16 codes, bits <= 11; ``self.engine`` "mfma") or the VALU engine
                    (int16 codes, ``self.engine`` "valu") -- bit-identical results
       "depthwise"  groups == C_in == C_out, weight bits <= 22: tq_ops.tr_dwconv2d
+      "wide"       groups == 1, weight bits 15-16 (the (16, 1, 16) squeeze-excite convs of
+                   EfficientNet-b0): tq_ops.tr_conv2d_wide, int32 weight codes, int64 sums
       "reference"  anything else: the reference composition self.conv(self.input_quant(x))
                    with the HIP TR op (``self.termpair`` is True only for "termpair").
     The term-pair kernels are GPU kernels: a CPU input (the MNIST CPU config)
@@ -213,8 +225,14 @@ class TRConv2dLayer(nn.Module):
         elif (plain and c.groups > 1 and c.groups == c.in_channels == c.out_channels
               and weight_bits <= 22):
             mode = "depthwise"
+        elif plain and c.groups == 1 and weight_bits <= tq_ops.MAX_WIDE_WEIGHT_BITS:
+            mode = "wide"
         packed = None
-        if mode != "reference":
+        if mode == "wide":
+            wq, codes = tq_ops.tr_encode(w.detach().contiguous(), self.w_sf, weight_bits,
+                                         group_size, num_terms)
+            packed, cp = tq_ops.pack_wide_weight(codes)
+        elif mode != "reference":
             wq, codes = tq_ops.tr_encode(w.detach().contiguous(), self.w_sf, weight_bits,
                                          group_size, num_terms)
             # int32 accumulator bound: sum_k |v_w| * max|v_x| (|v_x| <= 2^data_bits)
@@ -262,6 +280,11 @@ class TRConv2dLayer(nn.Module):
         if any(pad):
             # TR(0) == 0: zero-padding before the encode equals padding the TR'd input
             x = torch.nn.functional.pad(x, (pad[2], pad[3], pad[0], pad[1]))
+        if self.mode == "wide":
+            return tq_ops.tr_conv2d_wide(x, self.input_quant.sf, self.data_bits,
+                                         self.data_terms, self.w_codes, self.act_channels,
+                                         self.w_sf, c.bias, c.out_channels, c.kernel_size,
+                                         c.stride, c.padding, c.dilation)
         return tq_ops.tr_conv2d(x, self.input_quant.sf, self.data_bits, self.data_terms,
                                 self.w_codes, self.act_channels, self.w_sf, c.bias,
                                 c.out_channels, c.kernel_size, c.stride, c.padding, c.dilation,

@@ -111,3 +111,43 @@ def test_ops_reject_other_devices_like_the_reference():
         tq_ops.tr(torch.zeros(2, 4, device="meta"), 1.0, 8, 1, 1)
     with pytest.raises(RuntimeError, match="CUDA"):
         tq_ops.tr_elementwise(torch.zeros(2, 4, device="meta"), 1.0, 8, 1)
+
+
+def test_histc_argument_validation():
+    lib = tq_native.lib()
+    buf = 16  # a fake, aligned, non-null address: every call below fails validation first
+    assert lib.tq_histc_f32(buf, 8, 0, -50.0, 50.0, buf, buf, None) == 1
+    assert b"nbins" in lib.tq_last_error()
+    assert lib.tq_histc_f32(buf, 8, 8192, 50.0, 50.0, buf, buf, None) == 1
+    assert b"min < max" in lib.tq_last_error()
+    assert lib.tq_histc_f32(buf, 8, 8192, -50.0, 50.0, None, buf, None) == 1
+    assert b"null" in lib.tq_last_error()
+    assert lib.tq_histc_f32(18, 8, 8192, -50.0, 50.0, buf, buf, None) == 1
+    assert b"aligned" in lib.tq_last_error()
+
+
+def test_conv_f16_fused_downsample_validation():
+    lib = tq_native.lib()
+    out = ctypes.c_void_p(16)
+    args = (None, 2, 8, 8, 64, None, 64, 3, 3, 576, 1, 1, 1, 1, 1, 1, 1.0, None, out, 8, 8, 1,
+            0, -1)
+
+    def run(**kw):
+        epi = tq_native.ConvEpilogue()
+        epi.ds_codes, epi.ds_w_codes, epi.ds_scale, epi.ds_shift = 16, 16, 16, 16
+        epi.ds_h, epi.ds_w, epi.ds_cp, epi.ds_stride = 16, 16, 64, 2
+        for k, v in kw.items():
+            setattr(epi, k, v)
+        return lib.tq_conv2d_termpair_f16(*args, ctypes.byref(epi), None)
+
+    assert run(residual=16) == 1 and b"replaces the residual" in lib.tq_last_error()
+    assert run(ds_w_codes=None) == 1 and b"weights" in lib.tq_last_error()
+    assert run(ds_cp=32) == 1 and b"shape" in lib.tq_last_error()
+    assert run(ds_h=14) == 1 and b"size mismatch" in lib.tq_last_error()
+    assert run(ds_codes=24) == 1 and b"aligned" in lib.tq_last_error()
+    assert run(split_k=-1) == 2 and b"data-parallel" in lib.tq_last_error()
+    epi = tq_native.ConvEpilogue()
+    epi.ds_codes = 16
+    rc = lib.tq_conv2d_termpair_fused(None, 2, 8, 8, 64, None, 64, 3, 3, 576, 1, 1, 1, 1, 1, 1,
+                                      1.0, None, out, 8, 8, ctypes.byref(epi), None)
+    assert rc == 2 and b"MFMA" in lib.tq_last_error()

@@ -273,3 +273,65 @@ def test_stem_bn_relu_maxpool_encode(dtype):
     yq = oracle.tr(out.contiguous().cpu().numpy().reshape(1, -1, 1, 1), 0.05, 9, 1, 3)
     exp = np.rint(yq.reshape(out.shape) / np.float32(0.05)).astype(np.int64)
     assert torch.equal(codes.cpu().long().permute(0, 3, 1, 2), torch.from_numpy(exp))
+
+
+@pytest.mark.parametrize("cin,cout,hw,n", [(64, 128, 28, 3), (128, 256, 14, 2), (256, 512, 7, 5),
+                                           (64, 64, 9, 1)])
+@pytest.mark.parametrize("kc", [0, 2])
+def test_fused_downsample_phase_bit_identical(cin, cout, hw, n, kc, monkeypatch):
+    """conv2 with the downsample as a second accumulation phase (tq_conv_epilogue.ds_*) equals
+    conv2 with the separate downsample conv's stored identity as its residual, bit for bit:
+    fp32 output and next-layer codes (partial pixel tiles, odd batches, a flushing main conv)."""
+    monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
+    monkeypatch.setenv("TQ_FUSE_DS", "1")
+    conv2_l, bn2 = _layer(cout, cout, 3, 1, seed=cout)
+    down_l, bnd = _layer(cin, cout, 1, 2, seed=cin + 1)
+    down_l.input_quant.sf = 0.04
+    conv2 = tq_fuse._Conv(conv2_l, bn2, nonneg=True)
+    if kc:
+        conv2.kc_steps = kc  # force the flushing main loop (a smaller window stays exact)
+    down = tq_fuse._Conv(down_l, bnd, nonneg=True)
+    assert conv2.fusable_downsample(down)
+    nxt, _ = _layer(cout, cout, 3, 1, seed=5)
+    nxt.input_quant.sf = 0.05
+    nxt_conv = tq_fuse._Conv(nxt, None, nonneg=True)
+    torch.manual_seed(3)
+    mid_x = torch.relu(torch.randn(n, cout, hw, hw, device=DEV))
+    in_x = torch.relu(torch.randn(n, cin, 2 * hw, 2 * hw, device=DEV))
+    mid = torch.empty((n, hw, hw, conv2.cp_in), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(mid_x.contiguous(memory_format=torch.channels_last), True, 0.03, 9, 3,
+                         mid)
+    dcodes = torch.empty((n, 2 * hw, 2 * hw, down.cp_in), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(in_x.contiguous(memory_format=torch.channels_last), True, 0.04, 9, 3,
+                         dcodes)
+    identity, _, _ = down(dcodes, out=True)
+    y_sep, c_sep, _ = conv2(mid, out=True, residual=identity, relu=True, next_a=nxt_conv)
+    y_fus, c_fus, _ = conv2(mid, out=True, relu=True, next_a=nxt_conv,
+                            downsample=(down, dcodes))
+    assert torch.equal(y_sep, y_fus)
+    assert torch.equal(c_sep.view(torch.int16), c_fus.view(torch.int16))
+    assert (y_fus > 0).any()
+
+
+def test_fused_resnet_downsample_phase(monkeypatch):
+    """The executor with each transition block's downsample fused into its conv2 gives the same
+    logits, bit for bit, as with separate downsample launches."""
+    monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
+    monkeypatch.setenv("TQ_FUSE_DS", "1")
+    torch.manual_seed(0)
+    model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(6, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        q(x)
+    tr_layer.set_tr_tracking(q, False)
+    fused = tq_fuse.FusedResNet(q)
+    downs = [b for b in fused.blocks if b.down is not None]
+    assert len(downs) == 3 and all(b.conv2.fusable_downsample(b.down) for b in downs)
+    with torch.no_grad():
+        one = fused(x)
+        monkeypatch.setenv("TQ_FUSE_DS", "0")
+        assert not downs[0].conv2.fusable_downsample(downs[0].down)
+        two = fused(x)
+    assert torch.equal(one, two)

@@ -62,6 +62,49 @@ def test_depthwise_termpair_matches_reference(cfg, channels_last):
     _check(y, ref, mag)
 
 
+@pytest.mark.parametrize("cfg", [
+    # cin, cout, k, stride, pad, hw, batch, bias, static-same
+    (1152, 48, 1, 1, 0, 1, 256, True, True),    # EfficientNet-b0 squeeze-excite reduce
+    (48, 1152, 1, 1, 0, 1, 256, True, True),    # ... and expand
+    (20, 70, 3, 2, 1, 9, 3, False, False),      # general shape: taps, stride, padding
+    (96, 24, 5, 1, 0, 12, 2, True, True),       # static "same" padding, 5x5
+])
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_wide_termpair_matches_reference(cfg, channels_last):
+    """groups = 1 convs with (16, 1, 16) weights (int32 codes, int64 sums) against
+    conv2d_fp64(TR(x), TR(w)) + bias, TR'd by the oracle; activations of both signs (the SE
+    convs see swish outputs)."""
+    cin, cout, k, s, p, hw, n, bias, same = cfg
+    torch.manual_seed(cin + cout + k)
+    if same:
+        conv = Conv2dStaticSamePadding(cin, cout, k, stride=s, bias=bias, image_size=hw)
+    else:
+        conv = nn.Conv2d(cin, cout, k, s, p, bias=bias)
+    w = conv.weight.detach().clone()
+    b = conv.bias.detach().clone() if bias else None
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 16, 1, 16)
+    assert layer.mode == "wide"
+    layer.input_quant.tracking = False
+    layer.input_quant.sf = 0.01
+    x = torch.randn(n, cin, hw, hw)
+    xd = x.to(DEV)
+    if channels_last:
+        xd = xd.to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = layer(xd)
+    xq = _tr_x(x, 0.01, 9, 3)
+    wq = torch.from_numpy(oracle.tr(w.numpy(), layer.w_sf, 16, 1, 16)).double()
+    assert torch.equal(layer.conv.weight.detach().cpu().double(), wq)
+    assert float(wq.abs().max() / np.float32(layer.w_sf)) > 2**14  # codes leave int16 range
+    if same:
+        xq = conv.static_padding.cpu()(xq)
+    ref = F.conv2d(xq, wq, b.double() if bias else None, s, conv.padding)
+    mag = F.conv2d(xq.abs(), wq.abs(), None, s, conv.padding)
+    assert y.shape == ref.shape
+    assert y.is_contiguous(memory_format=torch.channels_last) == channels_last or hw == 1
+    _check(y, ref, mag)
+
+
 def test_linear_termpair_matches_reference():
     torch.manual_seed(3)
     lin = nn.Linear(650, 300)
@@ -132,3 +175,6 @@ def test_depthwise_models_layers_match_reference_composition(arch):
     for h in hooks:
         h.remove()
     assert {"termpair", "depthwise"} <= modes
+    assert "reference" not in modes  # every converted layer runs a term-pair kernel
+    if arch == "efficientnet_b0":
+        assert "wide" in modes  # the (16, 1, 16) squeeze-excite convs

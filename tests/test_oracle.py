@@ -150,3 +150,21 @@ def test_oracle_ubsan_clean(tmp_path):
     r = subprocess.run(["python", "-c", code], capture_output=True)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     assert b"runtime error" not in r.stderr
+
+
+@pytest.mark.parametrize("nbins,minv,maxv", [(8192, -50, 50), (1000, -3, 7), (37, 0, 1)])
+def test_oracle_histc_matches_torch_histc(nbins, minv, maxv):
+    """The histogram restatement behind the tracking-kernel tests equals torch.histc (the
+    reference's call, tr_layer.py:91-94) on random values, every bin edge and its fp32
+    neighbours, the range ends, out-of-range values, infinities and NaN."""
+    import torch
+    rng = np.random.default_rng(nbins)
+    lo, hi = np.float32(minv), np.float32(maxv)
+    edges = (lo + np.arange(nbins + 1, dtype=np.float32) * ((hi - lo) / np.float32(nbins)))
+    x = np.concatenate([
+        rng.standard_normal(1 << 16).astype(np.float32) * (hi - lo) / 2 + (hi + lo) / 2,
+        edges, np.nextafter(edges, np.float32(-np.inf)), np.nextafter(edges, np.float32(np.inf)),
+        np.array([lo, hi, np.inf, -np.inf, np.nan, 1e30, -1e30], np.float32)]).astype(np.float32)
+    got = oracle.histc(x, nbins, minv, maxv)
+    exp = torch.histc(torch.from_numpy(x), nbins, minv, maxv).numpy().astype(np.int64)
+    np.testing.assert_array_equal(got, exp)

@@ -28,8 +28,49 @@ sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
 import cnn_models  # noqa: E402
 import evaluate_lstm  # noqa: E402
 import profile_model  # noqa: E402
+import tq_ops  # noqa: E402
 import tr_layer  # noqa: E402
 from lstm_models import model as model_mod  # noqa: E402
+
+sys.path.insert(0, ROOT)
+from bench import HBM_PEAK_GBS, MFMA_F16_PEAK_TFLOPS, KernelTimer  # noqa: E402
+
+
+def kernel_breakdown(fn, steps, total_s):
+    """A second pass of `steps` steps with HIP events around every TQ kernel (tq_ops hook, as
+    bench.py): per kernel family launches, average duration, share of the step and its
+    roofline -- term-pair MFMA convs against the dense fp16 MFMA peak (2 FLOP per term-sum
+    product), the HBM-bound kernels (activation encode, depthwise) against 8 TB/s with
+    their algorithmic bytes."""
+    timer = KernelTimer()
+    tq_ops.set_kernel_hook(timer)
+    try:
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+    finally:
+        tq_ops.set_kernel_hook(None)
+    out = {}
+    for name, k in timer.summary().items():
+        e = {"launches_per_step": k["launches"] // steps,
+             "avg_launch_us": k["seconds"] / k["launches"] * 1e6,
+             "share_of_step": k["seconds"] / steps / total_s}
+        if name == "conv2d_termpair":
+            tf = 2 * k["work"] / k["seconds"] / 1e12
+            e.update({"bound": "mfma", "achieved_tflops": tf, "peak_tflops": MFMA_F16_PEAK_TFLOPS,
+                      "frac": tf / MFMA_F16_PEAK_TFLOPS})
+        elif name in ("act_encode",):
+            gbs = k["work"] / k["seconds"] / 1e9
+            e.update({"bound": "hbm", "achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
+                      "frac": gbs / HBM_PEAK_GBS})
+        else:  # depthwise / wide term-pair kernels: work = term-sum products
+            e.update({"term_sum_macs_per_s": k["work"] / k["seconds"]})
+            if k["bytes"]:  # depthwise: HBM-bound (codes in, fp32 out, once each)
+                gbs = k["bytes"] / k["seconds"] / 1e9
+                e.update({"bound": "hbm", "achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
+                          "frac": gbs / HBM_PEAK_GBS})
+        out[name] = e
+    return out
 
 
 def timed(fn, steps, warmup):
@@ -58,10 +99,31 @@ def lstm(args, dev):
         tmacs, _ = profile_model.get_model_ops(q, inputs=(x, model.init_hidden(bsz)))
         hidden = model.init_hidden(bsz)
         t = timed(lambda: q(x, hidden), args.steps, args.warmup)
+        # the decoder as a term-pair GEMM (TRLinearLayer(quantize_input=True): linear(TR(h),
+        # TR(W)) on the MFMA engine), timed alone on the 350 x 650 LSTM output
+        dec = torch.nn.Linear(650, ntokens).to(dev)
+        dec.weight.data.copy_(model.decoder.weight.data)
+        dec.bias.data.copy_(model.decoder.bias.data)
+        tpl = tr_layer.TRLinearLayer(dec, 8, 8, 8, 8, 12, quantize_input=True)
+        h = torch.randn(bptt * bsz, 650, device=dev).tanh()
+        tpl(h)
+        tpl.tracking(False)
+        td = timed(lambda: tpl(h), args.steps, args.warmup)
     toks = bptt * bsz
+    dec_macs = toks * 650 * ntokens
     return {"metric": "LSTM-650 TQ tokens/s", "value": toks / t, "unit": "tokens/s",
-            "ms_per_step": t * 1e3, "term_pair_macs_per_step": tmacs,
-            "term_pair_macs_per_s": tmacs / t,
+            "ms_per_step": t * 1e3,
+            # profile_model's count (the published metric) is analytic: this forward keeps the
+            # reference's semantics (TRLSTMLayer: fp32 MIOpen LSTM on TR'd weights / quantized
+            # inputs; TRLinearLayer: dense decoder on the unquantized input), no term-pair kernel
+            "analytic_term_pair_macs_per_step": tmacs,
+            "analytic_term_pair_macs_per_s": tmacs / t,
+            "term_pair_decoder": {
+                "what": "TRLinearLayer(quantize_input=True) 650 -> %d on %d rows, term-pair "
+                        "GEMM on the MFMA engine, timed alone" % (ntokens, toks),
+                "ms": td * 1e3, "term_sum_products": dec_macs,
+                "achieved_tflops": 2 * dec_macs / td / 1e12,
+                "frac_of_fp16_mfma_peak": 2 * dec_macs / td / 1e12 / MFMA_F16_PEAK_TFLOPS},
             "config": {"workload": "lstm-650 wikitext-2 vocab, g=8 k=12 wb=db=dt=8",
                        "batch": bsz, "bptt": bptt, "data": "synthetic token ids"}}
 
@@ -78,13 +140,15 @@ def cnn(arch, args, dev):
         q(x)
         tr_layer.set_tr_tracking(q, False)
         t = timed(lambda: q(x), args.steps, args.warmup)
+        kernels = kernel_breakdown(lambda: q(x), args.steps, t)
     modes = sorted({m.mode for m in q.modules() if isinstance(m, tr_layer.TRConv2dLayer)})
     return {"metric": "%s TQ images/s" % arch, "value": args.batch / t, "unit": "images/s",
             "ms_per_step": t * 1e3, "term_pair_macs_per_image": tmacs,
             "term_pair_macs_per_s": tmacs * args.batch / t,
             "config": {"workload": "%s-tq (dw wb=16 g=1 k=16; others g=8 k=12 wb=db=9 dt=3)"
                                    % arch, "batch": args.batch, "layer_modes": modes,
-                       "data": "synthetic N(0,1), random-init weights"}}
+                       "data": "synthetic N(0,1), random-init weights"},
+            "kernels": kernels}
 
 
 def main():
