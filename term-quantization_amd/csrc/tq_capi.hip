@@ -3,6 +3,7 @@
 // the calls are capturable in a hipGraph.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/tq.h"
 #include "tq_device.h"
@@ -201,6 +202,17 @@ int code_target(const void* codes, int64_t cp, float sf, int32_t bits, int32_t t
 }
 
 // Fill the fused-epilogue fields of `a` from `epi` (shared by both conv engines).
+// Entries of an epilogue code table (tq_device.h kLutMax) for one code target: maxv + 1 when
+// the ReLU fast path applies (relu, 0 < sf < inf) and maxv < kLutMax, else 0 (the kernels
+// compute the codes).  TQ_LUT=0 turns the tables off (A/B, tools only).
+int lut_entries(bool codes, bool relu, double inv, float maxv) {
+  static const char* env = getenv("TQ_LUT");
+  if (env && atoi(env) == 0) return 0;
+  if (!codes || !relu || !(inv > 0.0 && inv <= 1.0e308)) return 0;
+  const int n = (int)maxv + 1;
+  return n <= tq::kLutMax ? n : 0;
+}
+
 int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int num_configs,
                    tq::ConvArgs* a) {
   if (cout % 4 != 0)
@@ -235,6 +247,8 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
   a->k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
   a->fmt_b = epi->fmt_b;
+  a->lut_a = lut_entries(a->codes_a != nullptr, a->relu != 0, a->inv_a, a->maxv_a);
+  a->lut_b = lut_entries(a->codes_b != nullptr, a->relu != 0, a->inv_b, a->maxv_b);
   if (epi->config < 0 || epi->config > num_configs || epi->split_k < -1 || epi->split_k > 64)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
   if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
@@ -486,6 +500,9 @@ int tq_stem_conv_pool_encode(const float* x, int64_t n, int64_t h, int64_t w,
   a.inv_b = 1.0 / (double)sf_b;
   a.maxv_b = (float)((1u << (codes_b ? bits_b : 0)) - 1u);
   a.k_b = terms_b < 0 ? 0 : terms_b;
+  // the pooled outputs are ReLU'd: the epilogue code tables apply
+  a.lut_a = lut_entries(codes_a != nullptr, true, a.inv_a, a.maxv_a);
+  a.lut_b = lut_entries(codes_b != nullptr, true, a.inv_b, a.maxv_b);
   const hipError_t e = tq::launch_stem_conv_pool(a, (hipStream_t)stream);
   if (e == hipErrorInvalidConfiguration)
     return fail(TQ_ERR_UNSUPPORTED, "stem_conv_pool: image too wide for the LDS tile");

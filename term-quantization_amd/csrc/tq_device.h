@@ -152,6 +152,18 @@ __device__ __forceinline__ int relu_peels(float maxv, int k) {
   return k < hese_max_terms(bw) ? k : hese_max_terms(bw);
 }
 
+// Epilogue code table.  On the ReLU fast path (y >= 0, 0 < sf < inf) the next layer's code is
+// a function of the quantized magnitude q alone, so each workgroup builds code[q] for q <=
+// maxv once in LDS (tr_value_of_q -> code bits) and an epilogue value costs the a1 rounding
+// plus one ds_read_u16 instead of the HESE masks, the top-bit peels and the conversion to the
+// code format (about 20 VALU per value).  Tables cover bit widths <= 11 (the MFMA code range).
+constexpr int kLutMax = 2048;
+
+__device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
+  const float r = fminf(quotient_f32(y, inv_sf), maxv);
+  return (uint32_t)r + (__builtin_amdgcn_fractf(r) >= 0.5f ? 1u : 0u);
+}
+
 // Activation / weight code formats of the term-pair kernels (include/tq.h TQ_CODES_*):
 // the same signed integer term sum v stored as int16 (VALU dot2 engine) or as the fp16
 // value v (MFMA engine; exact for |v| <= 2048, i.e. bitwidth <= 11).
@@ -163,6 +175,14 @@ __device__ __forceinline__ uint32_t code_bits(int32_t v, int fmt) {
   // (v_cvt_f16_i16, one rounding) equals the int32 -> fp16 one
   return fmt == kCodesF16 ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(int16_t)v)
                           : ((uint32_t)v & 0xFFFFu);
+}
+
+// code[q] = code bits of TR(q * sf) for q in [0, n) (k >= 0 kept terms), by the threads of a
+// workgroup; visible after the caller's next barrier.
+__device__ __forceinline__ void lut_build(uint16_t* lut, int n, int k, int fmt, int tid,
+                                          int nthreads) {
+  for (int q = tid; q < n; q += nthreads)
+    lut[q] = (uint16_t)code_bits(tr_value_of_q((uint32_t)q, k, false), fmt);
 }
 
 }  // namespace tq

@@ -37,9 +37,13 @@ __device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4
 // into NaN in its fp32 window.
 __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, int64_t p, int co,
                                              const float y[4], double inv_sf, float maxv,
-                                             int k, int fmt, bool relu) {
+                                             int k, int fmt, bool relu,
+                                             const uint16_t* lut = nullptr) {
   uint32_t v[4];
-  if (relu && inv_sf > 0.0 && inv_sf <= 1.0e308) {  // y >= 0, 0 < sf < inf: fast path
+  if (lut) {  // the fast path's codes from the LDS table (set only where it applies)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = lut[relu_q(y[i], inv_sf, maxv)];
+  } else if (relu && inv_sf > 0.0 && inv_sf <= 1.0e308) {  // y >= 0, 0 < sf < inf: fast path
     int32_t t[4];
     tr_values_relu4(y, inv_sf, maxv, relu_peels(maxv, k), t);
 #pragma unroll
@@ -59,7 +63,9 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, i
 // output quad.  Cout % 4 == 0.
 __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int co,
                                                const int acc[4], const double sc[4],
-                                               const double sh[4], const float4 rv) {
+                                               const double sh[4], const float4 rv,
+                                               const uint16_t* lut_a = nullptr,
+                                               const uint16_t* lut_b = nullptr) {
   float y[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
@@ -81,9 +87,9 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
   if (a.out)
     *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(o[0], o[1], o[2], o[3]);
   if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
-                               a.relu);
+                               a.relu, lut_a);
   if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
-                               a.relu);
+                               a.relu, lut_b);
 }
 
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
@@ -91,7 +97,9 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
 // (tr_layer.py:96-99 applied to the stored value).
 __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
                                            const int acc[4], const double sc[4],
-                                           const double sh[4], bool vec) {
+                                           const double sh[4], bool vec,
+                                           const uint16_t* lut_a = nullptr,
+                                           const uint16_t* lut_b = nullptr) {
   float y[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
@@ -129,9 +137,24 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
     }
   }
   if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
-                               a.relu);
+                               a.relu, lut_a);
   if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
-                               a.relu);
+                               a.relu, lut_b);
+}
+
+// Epilogue code tables of a conv launch in LDS at `base` (a.lut_a then a.lut_b entries),
+// built by the workgroup's threads; the caller's next barrier makes them visible.
+__device__ __forceinline__ void conv_luts(const ConvArgs& a, uint16_t* base, uint16_t*& la,
+                                          uint16_t*& lb) {
+  la = a.lut_a ? base : nullptr;
+  lb = a.lut_b ? base + a.lut_a : nullptr;
+  const int nt = blockDim.x;
+  if (la) lut_build(la, a.lut_a, a.k_a, a.fmt_a, threadIdx.x, nt);
+  if (lb) lut_build(lb, a.lut_b, a.k_b, a.fmt_b, threadIdx.x, nt);
+}
+
+__host__ __device__ inline int64_t conv_lut_bytes(const ConvArgs& a) {
+  return ((int64_t)(a.lut_a + a.lut_b) * 2 + 15) / 16 * 16;
 }
 
 // Bijective XCD-aware remap of the block index: blocks are dealt round-robin to the 8 XCDs

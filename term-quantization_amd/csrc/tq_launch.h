@@ -60,6 +60,10 @@ struct ConvArgs {
   const double* ds_scale;
   const double* ds_shift;
   int ds_H, ds_W, ds_Cp, ds_s;
+  // epilogue code tables (tq_device.h kLutMax): entries of codes_a's / codes_b's table
+  // (maxv + 1) when the ReLU fast path applies and it fits, else 0 (set by the C-ABI layer);
+  // a kernel that places them in LDS passes the LDS pointers to the emit functions
+  int lut_a, lut_b;
   int ab;  // timing-only A/B switches (TQ_AB, tools only; 0 in the product)
   int config, splits;
   int* ws;
@@ -104,6 +108,7 @@ struct PoolArgs {
   float sf_b, maxv_b;
   int fmt_a, fmt_b;
   double inv_a, inv_b;   // RN64(1 / sf_a), RN64(1 / sf_b)
+  int lut_a, lut_b;      // epilogue code table entries (as ConvArgs), 0 = none
   // fused stem (tq_stem_conv.hip): x is the [N][H][W][3] input image, H/W its size, and
   // wsplit the conv weights * 2^10 as two fp16 splits [2][64][192] (s2d K order)
   const uint16_t* wsplit;

@@ -86,6 +86,17 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(lds_raw) + kStemWBytes);
   // per-wave pool staging: 7 pixels x 64 channels fp32 behind the input rows
   float* pb = xs + (2 * TP + 4) * sc * 12 + (threadIdx.x >> 6) * (7 * 64);
+  // epilogue code tables behind the pool staging (the launcher sized the LDS for them or
+  // cleared lut_a / lut_b); visible after the first barrier
+  uint16_t* lut_a = a.lut_a ? reinterpret_cast<uint16_t*>(
+                                  xs + (2 * TP + 4) * sc * 12 + (kStemThreads / 64) * (7 * 64))
+                            : nullptr;
+  uint16_t* lut_b = a.lut_b ? reinterpret_cast<uint16_t*>(
+                                  xs + (2 * TP + 4) * sc * 12 + (kStemThreads / 64) * (7 * 64)) +
+                                  a.lut_a
+                            : nullptr;
+  if (lut_a) lut_build(lut_a, a.lut_a, a.k_a, a.fmt_a, threadIdx.x, kStemThreads);
+  if (lut_b) lut_build(lut_b, a.lut_b, a.k_b, a.fmt_b, threadIdx.x, kStemThreads);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -324,7 +335,11 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             const int cp = side ? a.cp_b : a.cp_a;
             const int fmt = side ? a.fmt_b : a.fmt_a;
             uint32_t v[4];
-            if (inv > 0.0 && inv <= 1.0e308) {  // yv >= 0 (ReLU, max), 0 < sf < inf: fast path
+            const uint16_t* lut = side ? lut_b : lut_a;
+            if (lut) {  // the fast path's codes from the LDS table
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[i] = lut[relu_q(yv[i], inv, maxv)];
+            } else if (inv > 0.0 && inv <= 1.0e308) {  // yv >= 0 (ReLU, max), 0 < sf < inf
               int32_t t[4];
               tr_values_relu4(yv, inv, maxv, relu_peels(maxv, k), t);
 #pragma unroll
@@ -360,9 +375,16 @@ template <int TP>
 hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   const int nb = (a.Wo + 6) / 7;
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
-  const int64_t bytes =
+  int64_t bytes =
       kStemWBytes + (int64_t)(2 * TP + 4) * sc * 12 * 4 + (kStemThreads / 64) * 7 * 64 * 4;
   if (bytes > kStemDynLds) return hipErrorInvalidConfiguration;
+  PoolArgs b = a;  // the epilogue code tables when they fit
+  const int64_t lut = ((int64_t)(a.lut_a + a.lut_b) * 2 + 15) / 16 * 16;
+  if (bytes + lut <= kStemDynLds) {
+    bytes += lut;
+  } else {
+    b.lut_a = b.lut_b = 0;
+  }
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP>),
@@ -377,7 +399,7 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
     cus = 256;
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return hipSuccess;
-  stem_conv_pool_kernel<TP><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(a, sc, nb,
+  stem_conv_pool_kernel<TP><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(b, sc, nb,
                                                                                  tiles);
   return hipGetLastError();
 }

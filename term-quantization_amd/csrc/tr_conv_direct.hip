@@ -62,6 +62,9 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
   __shared__ double coef[C::BM][2];  // epilogue (scale, shift) of the tile's channels
   __shared__ double coef2[DS ? C::BM : 1][2];  // the fused downsample's (scale, shift)
+  extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lut[];  // epilogue code tables
+  uint16_t *lut_a, *lut_b;
+  conv_luts(a, dyn_lut, lut_a, lut_b);  // read only after the epilogue's barrier
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = (a.Cout + C::BM - 1) / C::BM;
@@ -333,9 +336,9 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     const u32x4 v = t[px * C::SL + (slot ^ (px & 15))];
     const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
     if (vec)
-      emit4_nhwc_res(a, p, co, acc4, sc, sh, res[it]);
+      emit4_nhwc_res(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
-      emit4_nhwc(a, p, co, acc4, sc, sh, false);
+      emit4_nhwc(a, p, co, acc4, sc, sh, false, lut_a, lut_b);
   }
 }
 
@@ -343,7 +346,8 @@ template <int MB, bool FLUSH, bool DS>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   using C = DirCfg<MB>;
   const int64_t tiles = ((a.P + C::BN - 1) / C::BN) * ((a.Cout + C::BM - 1) / C::BM);
-  conv2d_tp_direct_kernel<MB, FLUSH, DS><<<dim3((unsigned)tiles), kDirThreads, 0, stream>>>(a);
+  conv2d_tp_direct_kernel<MB, FLUSH, DS>
+      <<<dim3((unsigned)tiles), kDirThreads, (size_t)conv_lut_bytes(a), stream>>>(a);
   return hipGetLastError();
 }
 

@@ -274,6 +274,9 @@ __global__ __launch_bounds__(pipe_threads(BM, BN), 1) void conv2d_tp_mfma_pipe_k
     ConvArgs a) {
   using C = PipeCfg<BM, BN, NS>;
   __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
+  extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lut[];  // epilogue code tables
+  uint16_t *lut_a, *lut_b;
+  conv_luts(a, dyn_lut, lut_a, lut_b);  // read only after the epilogue's barrier
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = (a.Cout + BM - 1) / BM;
   const int64_t ntn = (a.P + BN - 1) / BN;
@@ -429,7 +432,7 @@ __global__ __launch_bounds__(pipe_threads(BM, BN), 1) void conv2d_tp_mfma_pipe_k
       if (p >= a.P) continue;
       const u32x4 v = t[px * 16 + (slot ^ (px & 15))];
       const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-      emit4_nhwc(a, p, co, acc4, sc, sh, vec);
+      emit4_nhwc(a, p, co, acc4, sc, sh, vec, lut_a, lut_b);
     }
   }
 }
@@ -439,10 +442,22 @@ hipError_t launch_pipe_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
   using C = PipeCfg<BM, BN, NS>;
   const int64_t tiles = ((a.P + BN - 1) / BN) * ((a.Cout + BM - 1) / BM);
   const dim3 grid((unsigned)tiles);
+  ConvArgs b = a;
+  if ((int64_t)C::LDS * 16 + conv_lut_bytes(b) > 160 * 1024) b.lut_a = b.lut_b = 0;
+  const size_t dyn = out_nhwc ? (size_t)conv_lut_bytes(b) : 0;
+  if (!out_nhwc) b.lut_a = b.lut_b = 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kLutMax * 2);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
   if (out_nhwc)
-    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true><<<grid, C::THREADS, 0, stream>>>(a);
+    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true><<<grid, C::THREADS, dyn, stream>>>(b);
   else
-    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, false><<<grid, C::THREADS, 0, stream>>>(a);
+    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, false><<<grid, C::THREADS, 0, stream>>>(b);
   return hipGetLastError();
 }
 

@@ -79,11 +79,20 @@ __global__ __launch_bounds__(kPatchThreads, MB == 1 ? 4 : 2) void conv2d_tp_patc
   constexpr int BM = 64 * MB;                 // 2 waves x 32*MB Cout rows
   constexpr int AI = MB;                      // weight wave-instructions per wave and step
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  uint16_t *lut_a_, *lut_b_;
   const int PXS = a.patch_px;                 // patch slot pixels (multiple of 64)
   const int PI = PXS / 64;                    // patch wave-instructions per wave and chunk
   const int NPB = a.patch_bufs;
   u32x4* ring = lds;
   u32x4* patch = lds + NR * BM * 8;
+  // epilogue code tables behind both the K-loop images and the epilogue transpose
+  {
+    const int main_units = NR * BM * 8 + NPB * (PXS + 1) * 8;
+    const int epi_units = 8 * 64 * 8 * MB;
+    uint16_t* lt = reinterpret_cast<uint16_t*>(lds + (main_units > epi_units ? main_units
+                                                                             : epi_units));
+    conv_luts(a, lt, lut_a_, lut_b_);  // read only after the epilogue's barrier
+  }
 
   const int mt = (a.Cout + BM - 1) / BM;
   const int64_t ntn = (a.P + kPatchBN - 1) / kPatchBN;
@@ -405,7 +414,7 @@ __global__ __launch_bounds__(kPatchThreads, MB == 1 ? 4 : 2) void conv2d_tp_patc
 #if TQ_ABLATE == 7  // timing only: no epilogue stores (sums kept live)
         if (acc4[0] == 0x7fffffff && a.out) a.out[p] = (float)(sc[0] + sh[0]);
 #else
-        emit4_nhwc(a, p, co, acc4, sc, sh, vec);
+        emit4_nhwc(a, p, co, acc4, sc, sh, vec, lut_a_, lut_b_);
 #endif
       }
     }
@@ -521,8 +530,13 @@ hipError_t launch_patch_mb(ConvArgs a, int64_t px, hipStream_t stream) {
   static const char* env = getenv("TQ_PATCH_RING");  // A/B override (tools only)
   const int want = env ? atoi(env) : 5;
   for (int nr = want < 5 ? want : 5; nr >= 3; --nr) {
-    const int64_t bytes = patch_lds_bytes(MB, nr, a.patch_px, a.patch_bufs);
+    int64_t bytes = patch_lds_bytes(MB, nr, a.patch_px, a.patch_bufs);
     if (bytes < 0 || ntap < nr - 1) continue;
+    if (bytes + conv_lut_bytes(a) <= kLdsBytes) {
+      bytes += conv_lut_bytes(a);  // the epilogue code tables
+    } else {
+      a.lut_a = a.lut_b = 0;
+    }
     if (nr == 5) return launch_patch_sched<MB, 5>(a, bytes, stream);
     if (nr == 4) return launch_patch_sched<MB, 4>(a, bytes, stream);
     return launch_patch_sched<MB, 3>(a, bytes, stream);

@@ -54,6 +54,11 @@ constexpr int kStripMaxBlk = 4;     // 32-pixel blocks per wave (tile <= 8 block
 
 __host__ __device__ constexpr int strip_patch_px(int w) { return (kStripTR + 2) * w + 1; }
 
+// LDS bytes of a launch before the epilogue code tables (16-byte aligned).
+__host__ __device__ inline int64_t strip_lds_bytes(int64_t w) {
+  return ((int64_t)kStripWUnits + 2 * strip_patch_px((int)w) * 8 + 64) * 16 + 16;
+}
+
 // Wave-uniform team barrier through an LDS counter: every wave of the team adds 1, then
 // waits until the counter reaches `target` (4 per barrier).  The caller has already retired
 // what the others must see (vmcnt for its LDS-DMA, lgkmcnt for its LDS reads).  The spin is
@@ -87,7 +92,8 @@ constexpr int kStripDma = ((kStripTR + 2) * kStripMaxW * 8 / 64 + 3) / 4;
 template <bool RES, bool OUT, bool CB, bool FULL>
 __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& ep,
                                             const float acc4[4], const float rv[4], int P0,
-                                            int nvalid, float* outp, int16_t* ca, int16_t* cbp) {
+                                            int nvalid, float* outp, int16_t* ca, int16_t* cbp,
+                                            const uint16_t* lut_a, const uint16_t* lut_b) {
   float y[4], o[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -110,18 +116,27 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
     if (!codes) continue;
     const double inv = side ? a.inv_b : a.inv_a;
     const float maxv = side ? a.maxv_b : a.maxv_a;
-    int32_t v[4];
-    if (side ? ep.fast_b : ep.fast_a) {
-      tr_values_relu4(y, inv, maxv, side ? ep.npeel_b : ep.npeel_a, v);
-    } else {
-      const int k = side ? a.k_b : a.k_a;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = tr_value_g1_inv(y[e], inv, maxv, k);
-    }
+    const uint16_t* lut = side ? lut_b : lut_a;
     const int fmt = side ? a.fmt_b : a.fmt_a;
+    uint32_t bits[4];
+    if (lut) {  // the ReLU fast path's codes from the LDS table
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bits[e] = lut[relu_q(y[e], inv, maxv)];
+    } else {
+      int32_t v[4];
+      if (side ? ep.fast_b : ep.fast_a) {
+        tr_values_relu4(y, inv, maxv, side ? ep.npeel_b : ep.npeel_a, v);
+      } else {
+        const int k = side ? a.k_b : a.k_a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = tr_value_g1_inv(y[e], inv, maxv, k);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bits[e] = code_bits(v[e], fmt);
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      if (FULL || P0 + e < nvalid) codes[e * kStripC] = (int16_t)code_bits(v[e], fmt);
+      if (FULL || P0 + e < nvalid) codes[e * kStripC] = (int16_t)bits[e];
   }
 }
 
@@ -133,7 +148,8 @@ template <int NB, bool RES, bool OUT, bool CB, typename Refill>
 __device__ __forceinline__ void strip_tile(const ConvArgs& a, const u32x4* patch,
                                            const u32x4* wrow_ptr, int wkey, int W, int ZP,
                                            int pset, int r32, int hh, int co, int64_t pix0,
-                                           int nvalid, const StripEpi& ep, Refill refill) {
+                                           int nvalid, const StripEpi& ep, Refill refill,
+                                           const uint16_t* lut_a, const uint16_t* lut_b) {
   // ---- main loop: 9 taps x 4 substeps of 16 codes; fragments one substep ahead ----
   float16v acc[NB];
   int pp0[NB];
@@ -240,10 +256,12 @@ __device__ __forceinline__ void strip_tile(const ConvArgs& a, const u32x4* patch
       __builtin_amdgcn_sched_barrier(0);  // one group's loads and values live at a time
       if (full)
         strip_emit4<RES, OUT, CB, true>(a, ep, acc4, rv4, pl + 8 * q, nvalid, outp + off,
-                                   ca ? ca + off : nullptr, cbp ? cbp + off : nullptr);
+                                   ca ? ca + off : nullptr, cbp ? cbp + off : nullptr, lut_a,
+                                   lut_b);
       else
         strip_emit4<RES, OUT, CB, false>(a, ep, acc4, rv4, pl + 8 * q, nvalid, outp + off,
-                                    ca ? ca + off : nullptr, cbp ? cbp + off : nullptr);
+                                    ca ? ca + off : nullptr, cbp ? cbp + off : nullptr, lut_a,
+                                    lut_b);
     }
   }
   refill();
@@ -286,6 +304,11 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
   if (threadIdx.x < 16)
     lds[kStripWUnits + (threadIdx.x >> 3) * PX * 8 + ZP * 8 + (threadIdx.x & 7)] = (u32x4)0u;
   if (threadIdx.x < 2) reinterpret_cast<uint32_t*>(dummy + 64)[threadIdx.x] = 0u;
+  // epilogue code tables behind the counters (the launcher sized the LDS for them or
+  // cleared lut_a / lut_b)
+  uint16_t *lut_a, *lut_b;
+  conv_luts(a, reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(lds) + strip_lds_bytes(W)),
+            lut_a, lut_b);
 
   // patch DMA of tile t into this team's buffer: (TR + 2) * W pixels x 8 units, lane-linear;
   // always kStripDma instructions per wave (pieces past the patch go to the dummy slot)
@@ -368,13 +391,13 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
     const int co = 32 * cb + r32;
     switch (nb) {  // wave-uniform
       case 4: strip_tile<4, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
-                                          pix0, nv, ep, refill); break;
+                                          pix0, nv, ep, refill, lut_a, lut_b); break;
       case 3: strip_tile<3, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
-                                          pix0, nv, ep, refill); break;
+                                          pix0, nv, ep, refill, lut_a, lut_b); break;
       case 2: strip_tile<2, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
-                                          pix0, nv, ep, refill); break;
+                                          pix0, nv, ep, refill, lut_a, lut_b); break;
       case 1: strip_tile<1, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
-                                          pix0, nv, ep, refill); break;
+                                          pix0, nv, ep, refill, lut_a, lut_b); break;
       default: refill(); break;
     }
   }
@@ -382,9 +405,6 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
 
 }  // namespace
 
-int64_t strip_lds_bytes(int64_t w) {
-  return ((int64_t)kStripWUnits + 2 * strip_patch_px((int)w) * 8 + 64) * 16 + 16;
-}
 
 bool conv_strip_eligible(const ConvArgs& a, int out_nhwc) {
   return out_nhwc && a.Cp == kStripC && a.Cout == kStripC && a.KH == 3 && a.KW == 3 &&
@@ -412,8 +432,14 @@ hipError_t launch_strip_mode(const ConvArgs& a, hipStream_t stream) {
   const int64_t ntiles = (int64_t)a.N * ((a.Ho + kStripTR - 1) / kStripTR);
   int64_t grid = device_cus();
   if (grid > ntiles) grid = ntiles;
-  conv2d_tp_strip_kernel<RES, OUT, CB><<<dim3((unsigned)grid), kStripThreads,
-                                          (size_t)strip_lds_bytes(a.W), stream>>>(a, ntiles);
+  ConvArgs b = a;
+  int64_t bytes = strip_lds_bytes(a.W) + conv_lut_bytes(b);
+  if (bytes > 160 * 1024) {  // no room for the code tables: the computed fast path
+    b.lut_a = b.lut_b = 0;
+    bytes = strip_lds_bytes(a.W);
+  }
+  conv2d_tp_strip_kernel<RES, OUT, CB><<<dim3((unsigned)grid), kStripThreads, (size_t)bytes,
+                                          stream>>>(b, ntiles);
   return hipGetLastError();
 }
 
