@@ -328,7 +328,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     sc[i] = coef[4 * slot + i][0];
     sh[i] = coef[4 * slot + i][1];
   }
-#pragma unroll
+  // fully unrolled: res[] must stay in registers (a partial unroll indexes it in scratch)
+#pragma clang loop unroll(full)
   for (int it = 0; it < 32 / PXI; ++it) {
     const int px = it * PXI + lane / C::SL;
     const int64_t p = wn0 + px;
