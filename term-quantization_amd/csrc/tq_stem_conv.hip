@@ -27,7 +27,9 @@
 // oy-2..oy+1 and cols ox-2..ox+1, so K = 4 x 4 x 12 = 192 in the order (sy, sx, sub_r, sub_c,
 // c), and any 8 consecutive K values are 8 consecutive fp32 in an s2d row ([col][12] rows).
 //   LDS: weights [2 splits][64 rows of 208 fp16] (53 KB, staged once per workgroup) and
-//        the input tile as fp32 s2d rows [2TP+4][SC][12] (46 KB for TP = 2, W = 224)
+//        the input tile pre-split into two fp16 planes x0 = RN16(x), x1 = RN16(x - x0) of
+//        s2d rows [2TP+4][SC][12] each (the split of a value is done once, when its tile is
+//        staged, not per fragment read: every value feeds up to 16 taps x 4 Cout blocks)
 //   wave = one strip of 16 conv columns (7 pool columns) x 2TP+1 conv rows, two rows at a
 //        time; per row 6 K-steps x (4 Cout blocks x 3 split products)
 //        v_mfma_f32_16x16x32_f16, each weight fragment read once for both rows
@@ -57,17 +59,6 @@ constexpr int kStemWBytes = 2 * 64 * kStemWRow * 2;
 constexpr int kStemWExp = 10;   // weights are split as w * 2^10 (tq_ops.pack_stem_weight)
 constexpr int kStemXMag = 14;   // a tile's inputs are scaled to max |x| < 2^14
 constexpr int kStemDynLds = 160 * 1024 - 256;  // the rest of the CU's LDS: static tile_max
-
-// x = x0 + x1 + e: x0 = RN16(x), x1 = RN16(x - x0) (the remainder is exact in fp32: a
-// multiple of ulp32(x) below ulp16(x)); |e| <= 2^-22 |x| while x1 is a normal fp16.
-__device__ __forceinline__ void split2(const float (&x)[8], f16x8& x0, f16x8& x1) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 h0 = (_Float16)x[j];
-    x0[j] = h0;
-    x1[j] = (_Float16)(x[j] - (float)h0);
-  }
-}
 
 // __shfl_down(v, D, 16) as a DPP row shift (no LDS permute): lane i of each 16-lane row
 // reads lane i + D; lanes whose source is past the row end keep their own value.
@@ -150,22 +141,34 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       }
     }
   };
-  auto commit = [&](int kx) {  // rows scaled by 2^kx (exact while no underflow)
+  // The s2d tile is held pre-split: two fp16 planes x0 = RN16(x), x1 = RN16(x - x0) of the
+  // scaled inputs, each [2TP + 4][sc][12] (the bytes of the fp32 tile).  Every input value
+  // feeds up to 16 taps x 4 Cout blocks of MFMAs, so splitting it once here instead of per
+  // fragment read takes the split's VALU out of the main loop.
+  _Float16* xs0 = reinterpret_cast<_Float16*>(xs);
+  _Float16* xs1 = xs0 + (2 * TP + 4) * sc * 12;
+  auto commit = [&](int kx) {  // rows scaled by 2^kx (exact while no underflow), then split
+    auto put2 = [&](int e, float u, float v) {
+      const float xu = ldexpf(u, kx), xv = ldexpf(v, kx);
+      const _Float16 u0 = (_Float16)xu, v0 = (_Float16)xv;
+      const _Float16 u1 = (_Float16)(xu - (float)u0), v1 = (_Float16)(xv - (float)v0);
+      typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<f16x2*>(xs0 + e) = (f16x2){u0, v0};
+      *reinterpret_cast<f16x2*>(xs1 + e) = (f16x2){u1, v1};
+    };
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const int rid = wave + 8 * r;
       if (rid >= ROWS) continue;
-      float* row = xs + (rid >> 1) * sc * 12 + (rid & 1) * 6;
+      const int row = (rid >> 1) * sc * 12 + (rid & 1) * 6;
 #pragma unroll
       for (int q = 0; q < QMAX; ++q) {
         const int idx = lane + 64 * q;
         if (idx >= f4n) continue;
         // flat input-row float f -> s2d column 3 + f / 6, slot f % 6 of the sub row
         const int f = 4 * idx;
-        *reinterpret_cast<float2*>(row + (3 + f / 6) * 12 + f % 6) =
-            make_float2(ldexpf(pre[r][q].x, kx), ldexpf(pre[r][q].y, kx));
-        *reinterpret_cast<float2*>(row + (3 + (f + 2) / 6) * 12 + (f + 2) % 6) =
-            make_float2(ldexpf(pre[r][q].z, kx), ldexpf(pre[r][q].w, kx));
+        put2(row + (3 + f / 6) * 12 + f % 6, pre[r][q].x, pre[r][q].y);
+        put2(row + (3 + (f + 2) / 6) * 12 + (f + 2) % 6, pre[r][q].z, pre[r][q].w);
       }
     }
   };
@@ -222,15 +225,20 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       // BN + ReLU of conv rows (2*py0 - 1 + rr + r), r < NR, at column ox, channels
       // mb*16 + 4g + i.  Rows in pairs share every weight fragment read (LDS traffic), and
       // the input slices of step ks+1 are read during step ks's MFMAs.
-      auto load_x = [&](int rr, int ks, float (&xv)[8]) {
-        const int j = 4 * ks + g;  // 8-value K slice of this lane
+      // the lane's 8-value K slice of step ks at row rr, both split planes (8-byte aligned:
+      // slices start at multiples of 4 values)
+      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+      auto load_x = [&](int rr, int ks, f16x8& h0, f16x8& h1) {
+        const int j = 4 * ks + g;
         const int sy = j / 6;
         const int off = (j - sy * 6) * 8;
-        const float* src = xs + ((rr + sy) * sc + (ox + 1)) * 12 + off;
-        const float4 xa = *reinterpret_cast<const float4*>(src);
-        const float4 xb = *reinterpret_cast<const float4*>(src + 4);
-        xv[0] = xa.x; xv[1] = xa.y; xv[2] = xa.z; xv[3] = xa.w;
-        xv[4] = xb.x; xv[5] = xb.y; xv[6] = xb.z; xv[7] = xb.w;
+        const int e = ((rr + sy) * sc + (ox + 1)) * 12 + off;
+        const f16x4 a0 = *reinterpret_cast<const f16x4*>(xs0 + e);
+        const f16x4 b0 = *reinterpret_cast<const f16x4*>(xs0 + e + 4);
+        const f16x4 a1 = *reinterpret_cast<const f16x4*>(xs1 + e);
+        const f16x4 b1 = *reinterpret_cast<const f16x4*>(xs1 + e + 4);
+        h0 = __builtin_shufflevector(a0, b0, 0, 1, 2, 3, 4, 5, 6, 7);
+        h1 = __builtin_shufflevector(a1, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       };
       auto conv_rows = [&](auto nr_tag, int rr, f32x4 (&y)[2][4]) {
         constexpr int NR = decltype(nr_tag)::value;
@@ -239,18 +247,15 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         for (int r = 0; r < NR; ++r)
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) acc[r][mb] = (f32x4)0.0f;
-        float xc[NR][8], xn[NR][8];
+        f16x8 x0[NR], x1[NR], n0[NR], n1[NR];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) load_x(rr + r, 0, xc[r]);
+        for (int r = 0; r < NR; ++r) load_x(rr + r, 0, x0[r], x1[r]);
 #pragma unroll 1
         for (int ks = 0; ks < kStemK / 32; ++ks) {
           if (ks + 1 < kStemK / 32) {
 #pragma unroll
-            for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 1, xn[r]);
+            for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 1, n0[r], n1[r]);
           }
-          f16x8 x0[NR], x1[NR];
-#pragma unroll
-          for (int r = 0; r < NR; ++r) split2(xc[r], x0[r], x1[r]);
           {
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) {
@@ -268,9 +273,10 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           }
           }
 #pragma unroll
-          for (int r = 0; r < NR; ++r)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xc[r][e] = xn[r][e];
+          for (int r = 0; r < NR; ++r) {
+            x0[r] = n0[r];
+            x1[r] = n1[r];
+          }
         }
 #pragma unroll
         for (int r = 0; r < NR; ++r) {

@@ -30,6 +30,8 @@
 // (j, x) of the patch = input row r0 - 1 + j, column x; units swizzled ^ ((pix >> 1) & 7);
 // the extra pixel is all zeros and stands in for taps outside the image), then two team
 // counters.
+#include <stdlib.h>
+
 #include "tq_device.h"
 #include "tq_epilogue.h"
 #include "tq_launch.h"
@@ -406,6 +408,12 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
 }  // namespace
 
 
+// TQ_STRIP_RES=1 admits residual convs (A/B, tools only)
+static bool strip_res_ok() {
+  static const char* env = getenv("TQ_STRIP_RES");
+  return env && atoi(env) == 1;
+}
+
 bool conv_strip_eligible(const ConvArgs& a, int out_nhwc) {
   return out_nhwc && a.Cp == kStripC && a.Cout == kStripC && a.KH == 3 && a.KW == 3 &&
          a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.dh == 1 && a.dw == 1 &&
@@ -416,7 +424,7 @@ bool conv_strip_eligible(const ConvArgs& a, int out_nhwc) {
          // with a residual the lane-per-channel epilogue (one dword load + store per element)
          // measured slower than the direct engine's 4-channel vectors (218.7 vs 235.8 us,
          // profiles/r02_strip.md): block conv1s only
-         a.residual == nullptr && a.ds_x == nullptr;
+         (a.residual == nullptr || strip_res_ok()) && a.ds_x == nullptr;
 }
 
 template <bool RES, bool OUT, bool CB>
@@ -446,6 +454,9 @@ hipError_t launch_strip_mode(const ConvArgs& a, hipStream_t stream) {
 hipError_t launch_conv2d_strip(const ConvArgs& a, hipStream_t stream) {
   // no residual and no second code target (conv_strip_eligible); the RES instantiations
   // stay compilable for A/B work but are not launched
+  if (a.residual)
+    return a.out ? launch_strip_mode<true, true, false>(a, stream)
+                 : launch_strip_mode<true, false, false>(a, stream);
   return a.out ? launch_strip_mode<false, true, false>(a, stream)
                : launch_strip_mode<false, false, false>(a, stream);
 }
