@@ -305,6 +305,17 @@ int tq_mse_profile(const float *x, const float *hist, int64_t nbins, const float
                    void *stream);
 
 /*
+ * One step of an LSTM layer's point-wise update (torch.nn.LSTM gate order i, f, g, o), for the
+ * term-pair LSTM path of TRLSTMLayer (tr_layer.py:162-201, whose cuDNN LSTM runs on the TR'd
+ * layer-0 weights and quantized inputs): with gates = gx + hh ([b][4h], fp32),
+ *   c[b][j] <- sigmoid(f) * c[b][j] + sigmoid(i) * tanh(g),  h[b][j] = sigmoid(o) * tanh(c)
+ * gx = the step's input projection (TR(x) TR(W_ih)^T + b_ih, a term-pair GEMM), hh = the
+ * recurrent projection (h W_hh^T + b_hh).  c is updated in place; h may not alias gx / hh.
+ */
+int tq_lstm_cell_f32(const float *gx, const float *hh, float *c, float *h, int64_t batch,
+                     int64_t hidden, void *stream);
+
+/*
  * Tracking histogram of the activation calibration, replacing
  *   self.hist_bins += torch.histc(x, self.num_bins, self.minv, self.maxv)
  * of LinearQuantize.forward (tr_layer.py:91-94):

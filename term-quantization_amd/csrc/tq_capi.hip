@@ -574,6 +574,16 @@ int tq_conv2d_termpair_wide(const int16_t* act_codes, int64_t n, int64_t h, int6
   return hip_status(tq::launch_conv2d_wide(a, (hipStream_t)stream), "conv2d_wide launch");
 }
 
+int tq_lstm_cell_f32(const float* gx, const float* hh, float* c, float* h, int64_t batch,
+                     int64_t hidden, void* stream) {
+  if (batch < 0 || hidden < 0 || batch * hidden >= ((int64_t)1 << 40))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_cell: bad sizes");
+  if (batch * hidden > 0 && (!gx || !hh || !c || !h))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_cell: null pointer");
+  return hip_status(tq::launch_lstm_cell(gx, hh, c, h, batch, hidden, (hipStream_t)stream),
+                    "lstm_cell launch");
+}
+
 int tq_histc_f32(const float* x, int64_t numel, int64_t nbins, float minv, float maxv,
                  uint64_t* counts, float* hist, void* stream) {
   if (numel < 0 || nbins < 1 || nbins > (1 << 24))

@@ -94,6 +94,10 @@ struct WideConvArgs {
 
 hipError_t launch_conv2d_wide(const WideConvArgs& a, hipStream_t stream);
 
+// LSTM cell update (tq_lstm.hip): c, h [B][H] in place / out from gx, hh [B][4H]
+hipError_t launch_lstm_cell(const float* gx, const float* hh, float* c, float* h, int64_t B,
+                            int64_t H, hipStream_t stream);
+
 struct PoolArgs {
   const float* x;        // [N][H][W][C] fp32 (channels_last), C % 8 == 0
   const float* scale;    // [C] BN scale (gamma / sqrt(var + eps))

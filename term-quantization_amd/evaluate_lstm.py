@@ -24,7 +24,9 @@ from tr_layer import TRLinearLayer, TRLSTMLayer, set_tr_tracking
 WT2_VOCAB = 33278
 
 
-def replace_lstm_layers(model, tr_params, data_bits, data_terms):
+def replace_lstm_layers(model, tr_params, data_bits, data_terms, termpair=True):
+    """``termpair`` (an addition): TRLSTMLayer's term-pair layer-0 path (tr_layer.py; False =
+    the library LSTM on the TR'd tensors, the reference's literal composition)."""
     curr_layer = 0
     for name, layer in list(model.named_modules()):
         if isinstance(layer, (nn.Linear, nn.LSTM)):
@@ -36,7 +38,7 @@ def replace_lstm_layers(model, tr_params, data_bits, data_terms):
             weight_bits, group_size, weight_terms = tr_params[curr_layer]
             if isinstance(layer, nn.LSTM):
                 layer = TRLSTMLayer(layer, data_bits, data_terms, weight_bits,
-                                    group_size, weight_terms)
+                                    group_size, weight_terms, termpair=termpair)
             elif isinstance(layer, nn.Linear):
                 layer = TRLinearLayer(layer, data_bits, data_terms, weight_bits,
                                       group_size, weight_terms)
@@ -55,9 +57,9 @@ def static_lstm_layer_settings(model, weight_bits, group_size, num_terms):
     return stats
 
 
-def convert_model(model, tr_params, data_bits, data_terms):
+def convert_model(model, tr_params, data_bits, data_terms, termpair=True):
     model = deepcopy(model)
-    return replace_lstm_layers(model, tr_params, data_bits, data_terms)
+    return replace_lstm_layers(model, tr_params, data_bits, data_terms, termpair)
 
 
 def batchify(data, bsz, device):

@@ -49,6 +49,7 @@ _SIGNATURES = {
                            _vp],
     "tq_mse_profile": [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
     "tq_histc_f32": [_vp, _i64, _i64, _f32, _f32, _vp, _vp, _vp],
+    "tq_lstm_cell_f32": [_vp, _vp, _vp, _vp, _i64, _i64, _vp],
     "tq_conv2d_termpair_wide": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                 _i64, _i64, _i64, _i64, _i64, _i64, _f64, _vp, _vp, _i64, _i64,
                                 _i32, _vp],
@@ -301,6 +302,16 @@ def mse_profile(x, hist, sfs, bitwidth, num_keep_terms):
                                   int(bitwidth), int(num_keep_terms), _ptr(errs), _stream(x))
     _check(rc)
     return errs
+
+
+def lstm_cell(gx, hh, c, h):
+    """c <- sigmoid(f) c + sigmoid(i) tanh(g); h = sigmoid(o) tanh(c) for gates = gx + hh
+    (tq_lstm_cell_f32); gx, hh [B, 4H], c, h [B, H], contiguous fp32 CUDA tensors."""
+    b, hid = c.shape
+    with torch.cuda.device(c.device):
+        rc = lib().tq_lstm_cell_f32(_ptr(gx), _ptr(hh), _ptr(c), _ptr(h), b, hid, _stream(c))
+    _check(rc)
+    return h
 
 
 def histc_accumulate(x, hist, minv, maxv, counts):

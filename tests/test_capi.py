@@ -151,3 +151,11 @@ def test_conv_f16_fused_downsample_validation():
     rc = lib.tq_conv2d_termpair_fused(None, 2, 8, 8, 64, None, 64, 3, 3, 576, 1, 1, 1, 1, 1, 1,
                                       1.0, None, out, 8, 8, ctypes.byref(epi), None)
     assert rc == 2 and b"MFMA" in lib.tq_last_error()
+
+
+def test_lstm_cell_argument_validation():
+    lib = tq_native.lib()
+    assert lib.tq_lstm_cell_f32(None, None, None, None, 2, 3, None) == 1
+    assert b"null" in lib.tq_last_error()
+    assert lib.tq_lstm_cell_f32(None, None, None, None, -1, 3, None) == 1
+    assert lib.tq_lstm_cell_f32(None, None, None, None, 0, 3, None) == 0  # nothing to do

@@ -7,7 +7,9 @@ synthetic token ids, then one 35 x 10 chunk.
   * the shared quantizer's outputs on emb, h0 and c0 are bit-exact oracle.tr() (g = 1);
   * the log-probs are within 1e-5 of an fp64 CPU composition of the oracle-TR'd tensors
     (fp64 LSTM on TR(emb), TR(h0), TR(c0) with the TR'd layer-0 weights, decoder on the
-    unquantized LSTM output as the reference's TRLinearLayer does, log_softmax)."""
+    unquantized LSTM output as the reference's TRLinearLayer does, log_softmax).
+Both TRLSTMLayer paths: the reference composition (MIOpen LSTM) and ``termpair=True`` (layer
+0's input projection and first recurrent step as exact term-pair GEMMs, tq_lstm_cell_f32)."""
 import pytest
 import torch
 import torch.nn as nn
@@ -25,7 +27,8 @@ def _oracle_w(w, bits, g, k):
     return torch.from_numpy(oracle.tr(w.detach().cpu().contiguous().numpy(), sf, bits, g, k))
 
 
-def test_lstm650_tq_chunk_against_oracle():
+@pytest.mark.parametrize("termpair", [False, True])
+def test_lstm650_tq_chunk_against_oracle(termpair):
     import evaluate_lstm
     from lstm_models.model import RNNModel
     torch.manual_seed(1111)
@@ -34,9 +37,10 @@ def test_lstm650_tq_chunk_against_oracle():
     w_hh = model.rnn.weight_hh_l0.detach().clone()
     w_dec = model.decoder.weight.detach().clone()
     st = evaluate_lstm.static_lstm_layer_settings(model, 8, 8, 12)
-    q = evaluate_lstm.convert_model(model, st, 8, 8).eval()
+    q = evaluate_lstm.convert_model(model, st, 8, 8, termpair=termpair).eval()
     lstm = q.rnn
     assert isinstance(lstm, tr_layer.TRLSTMLayer)
+    assert lstm.termpair == termpair
     assert isinstance(q.decoder, tr_layer.TRLinearLayer)
     # weights: bit-exact, including the partial last group of every 650-wide row
     assert torch.equal(lstm.lstm.weight_ih_l0.detach().cpu(), _oracle_w(w_ih, 8, 8, 12))
@@ -64,7 +68,11 @@ def test_lstm650_tq_chunk_against_oracle():
         finally:
             h.remove()
     torch.cuda.synchronize()
-    # the shared quantizer ran on emb, h0, c0 (tr_layer.py:191-193): bit-exact
+    # the shared quantizer ran on emb, h0, c0 (tr_layer.py:191-193): bit-exact (the term-pair
+    # path encodes emb inside its term-pair GEMM: its quantizer call sees h0 and c0 only)
+    if termpair:
+        seen.insert(0, (q.encoder(data), tr_layer.tr_cuda.tr(
+            q.encoder(data).contiguous().view(1, -1, 1, 1), sf, 8, 1, 8).view(BPTT, BSZ, NHID)))
     assert len(seen) == 3
     for x, y in seen:
         exp = oracle.tr(x.detach().cpu().contiguous().numpy().reshape(1, -1, 1, 1), sf, 8, 1, 8)

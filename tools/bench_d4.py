@@ -89,7 +89,7 @@ def lstm(args, dev):
     ntokens, bsz, bptt = evaluate_lstm.WT2_VOCAB, 10, 35
     model = model_mod.RNNModel("LSTM", ntokens, 650, 650, 2, 0.5, True).to(dev).eval()
     tr_params = evaluate_lstm.static_lstm_layer_settings(model, 8, 8, 12)
-    q = evaluate_lstm.convert_model(model, tr_params, 8, 8)
+    q = evaluate_lstm.convert_model(model, tr_params, 8, 8, termpair=False)
     tokens = torch.randint(0, ntokens, (bptt * bsz * 4 + bsz,))
     data = evaluate_lstm.batchify(tokens, bsz, dev)
     x = evaluate_lstm.get_batch(data, 0, bptt)[0]
@@ -99,6 +99,12 @@ def lstm(args, dev):
         tmacs, _ = profile_model.get_model_ops(q, inputs=(x, model.init_hidden(bsz)))
         hidden = model.init_hidden(bsz)
         t = timed(lambda: q(x, hidden), args.steps, args.warmup)
+        # the same model with TRLSTMLayer(termpair=True) (the default): layer 0 on the
+        # term-pair kernels; `value` stays the MIOpen composition for comparability
+        qt = evaluate_lstm.convert_model(model, tr_params, 8, 8, termpair=True)
+        qt(x, model.init_hidden(bsz))
+        tr_layer.set_tr_tracking(qt, False)
+        t_tp = timed(lambda: qt(x, hidden), args.steps, args.warmup)
         # the decoder as a term-pair GEMM (TRLinearLayer(quantize_input=True): linear(TR(h),
         # TR(W)) on the MFMA engine), timed alone on the 350 x 650 LSTM output
         dec = torch.nn.Linear(650, ntokens).to(dev)
@@ -118,6 +124,7 @@ def lstm(args, dev):
             # inputs; TRLinearLayer: dense decoder on the unquantized input), no term-pair kernel
             "analytic_term_pair_macs_per_step": tmacs,
             "analytic_term_pair_macs_per_s": tmacs / t,
+            "termpair_lstm_tokens_per_s": toks / t_tp,
             "term_pair_decoder": {
                 "what": "TRLinearLayer(quantize_input=True) 650 -> %d on %d rows, term-pair "
                         "GEMM on the MFMA engine, timed alone" % (ntokens, toks),
