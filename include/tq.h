@@ -111,7 +111,8 @@ int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w
  *                                                       eval-mode BatchNorm folded, fp64)
  *     = fp32(acc * scale + bias[c])                    otherwise (plain conv)
  *   y = y + residual[p][c]            (fp32, if residual; [P][cout] channels_last)
- *   y = max(y, 0)                     (if relu; the stored out keeps a NaN, as torch.relu)
+ *   y = max(y, 0)                     (if relu == 1; the stored out keeps a NaN, as torch.relu)
+ *   y = min(max(y, 0), 6)             (if relu == 2: ReLU6, MobileNet-V2; NaN kept likewise)
  *   out[p][c] = y                     (if out)
  *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   format fmt_a, [P][cp_a] (if codes_a)
  *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   format fmt_b, [P][cp_b] (if codes_b)
@@ -251,6 +252,33 @@ int tq_conv2d_termpair_wide(const int16_t *act_codes, int64_t n, int64_t h, int6
                             int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
                             double scale, const float *bias, float *out, int64_t ho, int64_t wo,
                             int32_t out_nhwc, void *stream);
+
+/*
+ * Depthwise term-pair conv with a fused epilogue (MobileNet-V2's dw conv -> BN -> ReLU6 and
+ * the following project conv's input TR), channels_last:
+ *   y = fp32(acc * ch_scale[c] + ch_shift[c])   (folded eval BatchNorm, fp64)
+ *   y = max(y, 0) (relu 1) or min(max(y, 0), 6) (relu 2); out[p][c] = y (if out; NaN kept)
+ *   codes[p][c] = TR(y; sf, bits, terms) in format fmt, [p][cp] with the input's cp, pad
+ *   channels zero (if codes)
+ * Other arguments as tq_dwconv2d_termpair.
+ */
+typedef struct tq_dw_epilogue {
+  const double *ch_scale;
+  const double *ch_shift;
+  int32_t relu;
+  int16_t *codes;
+  int64_t cp;
+  float sf;
+  int32_t bits;
+  int32_t terms;
+  int32_t fmt;
+} tq_dw_epilogue;
+
+int tq_dwconv2d_termpair_fused(const int16_t *act_codes, int64_t n, int64_t h, int64_t w,
+                               int64_t c, int64_t cp, const int32_t *w_codes, int64_t kh,
+                               int64_t kw, int64_t stride_h, int64_t stride_w, int64_t pad_top,
+                               int64_t pad_left, int64_t dil_h, int64_t dil_w, float *out,
+                               int64_t ho, int64_t wo, const tq_dw_epilogue *epi, void *stream);
 
 /*
  * Stem tail of a TQ ResNet in one pass (the stem conv itself stays fp32, as in the

@@ -232,6 +232,8 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->ch_scale = epi->ch_scale;
   a->ch_shift = epi->ch_shift;
   a->residual = epi->residual;
+  if (epi->relu < 0 || epi->relu > 2)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: relu must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
   a->relu = epi->relu;
   a->codes_a = epi->codes_a;
   a->cp_a = (int)epi->cp_a;
@@ -357,11 +359,12 @@ int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int6
                     "conv2d_f16 launch");
 }
 
-int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t c,
-                         int64_t cp, const int32_t* w_codes, int64_t kh, int64_t kw,
-                         int64_t stride_h, int64_t stride_w, int64_t pad_top, int64_t pad_left,
-                         int64_t dil_h, int64_t dil_w, double scale, const float* bias,
-                         float* out, int64_t ho, int64_t wo, int32_t out_nhwc, void* stream) {
+static int dw_impl(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t c,
+                   int64_t cp, const int32_t* w_codes, int64_t kh, int64_t kw,
+                   int64_t stride_h, int64_t stride_w, int64_t pad_top, int64_t pad_left,
+                   int64_t dil_h, int64_t dil_w, double scale, const float* bias, float* out,
+                   int64_t ho, int64_t wo, int32_t out_nhwc, const tq_dw_epilogue* epi,
+                   void* stream) {
   if (n < 0 || h < 1 || w < 1 || c < 1 || kh < 1 || kw < 1 || ho < 1 || wo < 1)
     return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: bad shape");
   if (cp < c || cp % 8 != 0)
@@ -374,8 +377,9 @@ int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t
     return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: out must be 16-byte aligned");
   if (n * h * w * cp >= (int64_t)1 << 40 || kh * kw > 4096)
     return fail(TQ_ERR_UNSUPPORTED, "dwconv2d: problem too large");
-  if (out == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: out is null");
-  tq::DwConvArgs a;
+  if (out == nullptr && (epi == nullptr || epi->codes == nullptr))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: out is null");
+  tq::DwConvArgs a = tq::DwConvArgs();
   a.x = act_codes;
   a.w = w_codes;
   a.bias = bias;
@@ -397,7 +401,58 @@ int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t
   a.Wo = (int)wo;
   a.out_nhwc = out_nhwc ? 1 : 0;
   a.scale = scale;
+  if (epi) {
+    if (!out_nhwc)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: the fused epilogue is channels_last");
+    if ((epi->ch_scale == nullptr) != (epi->ch_shift == nullptr))
+      return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: ch_scale and ch_shift go together");
+    if (epi->relu < 0 || epi->relu > 2)
+      return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: relu must be 0, 1 or 2");
+    a.ch_scale = epi->ch_scale;
+    a.ch_shift = epi->ch_shift;
+    a.relu = epi->relu;
+    if (epi->codes) {
+      if (epi->cp != cp)
+        return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: the codes' cp must equal the input's");
+      if ((uintptr_t)epi->codes % 16 != 0)
+        return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: codes must be 16-byte aligned");
+      if (epi->fmt != TQ_CODES_I16 && epi->fmt != TQ_CODES_F16)
+        return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: bad code format");
+      if (epi->bits < 0 || epi->bits > max_code_bits(epi->fmt))
+        return fail(TQ_ERR_UNSUPPORTED, "dwconv2d: codes of %d bits do not fit the format",
+                    epi->bits);
+      if (!(epi->sf >= 0.0f))
+        return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: codes sf must be >= 0");
+      a.codes = epi->codes;
+      a.cp_c = (int)epi->cp;
+      a.k_c = epi->terms < 0 ? 0 : epi->terms;
+      a.fmt_c = epi->fmt;
+      a.inv_c = 1.0 / (double)epi->sf;
+      a.maxv_c = (float)((1u << epi->bits) - 1u);
+      a.lut_c = lut_entries(true, epi->relu != 0, a.inv_c, a.maxv_c);
+    }
+  }
   return hip_status(tq::launch_dwconv_tp(a, (hipStream_t)stream), "dwconv2d launch");
+}
+
+int tq_dwconv2d_termpair(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64_t c,
+                         int64_t cp, const int32_t* w_codes, int64_t kh, int64_t kw,
+                         int64_t stride_h, int64_t stride_w, int64_t pad_top, int64_t pad_left,
+                         int64_t dil_h, int64_t dil_w, double scale, const float* bias,
+                         float* out, int64_t ho, int64_t wo, int32_t out_nhwc, void* stream) {
+  return dw_impl(act_codes, n, h, w, c, cp, w_codes, kh, kw, stride_h, stride_w, pad_top,
+                 pad_left, dil_h, dil_w, scale, bias, out, ho, wo, out_nhwc, nullptr, stream);
+}
+
+int tq_dwconv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int64_t w,
+                               int64_t c, int64_t cp, const int32_t* w_codes, int64_t kh,
+                               int64_t kw, int64_t stride_h, int64_t stride_w, int64_t pad_top,
+                               int64_t pad_left, int64_t dil_h, int64_t dil_w, float* out,
+                               int64_t ho, int64_t wo, const tq_dw_epilogue* epi,
+                               void* stream) {
+  if (epi == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: epilogue is null");
+  return dw_impl(act_codes, n, h, w, c, cp, w_codes, kh, kw, stride_h, stride_w, pad_top,
+                 pad_left, dil_h, dil_w, 0.0, nullptr, out, ho, wo, 1, epi, stream);
 }
 
 int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, int64_t c,

@@ -81,6 +81,7 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
     o[i] = y[i];
     if (a.relu) {
       y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;  // ReLU6 (MobileNet-V2)
       o[i] = o[i] != o[i] ? o[i] : y[i];
     }
   }
@@ -123,6 +124,7 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
     o[i] = y[i];
     if (a.relu) {
       y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;  // ReLU6 (MobileNet-V2)
       o[i] = o[i] != o[i] ? o[i] : y[i];
     }
   }

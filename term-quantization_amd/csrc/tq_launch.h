@@ -74,9 +74,18 @@ struct DwConvArgs {
   const int16_t* x;     // activation codes [N][H][W][Cp]
   const int32_t* w;     // weight codes [KH*KW][Cp] (channel fastest)
   const float* bias;    // [C] or nullptr
-  float* out;           // [N][Ho][Wo][C] (out_nhwc) or [N][C][Ho][Wo]
+  float* out;           // [N][Ho][Wo][C] (out_nhwc) or [N][C][Ho][Wo]; nullptr = codes only
   int N, H, W, C, Cp, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo, out_nhwc;
   double scale;
+  // fused epilogue (NHWC only): y = fp32(acc * ch_scale[c] + ch_shift[c]) (folded BN),
+  // relu 1 = ReLU, 2 = ReLU6, then the next layer's codes [P][cp_c] = TR(y)
+  const double* ch_scale;
+  const double* ch_shift;
+  int relu;
+  int16_t* codes;
+  int cp_c, k_c, fmt_c, lut_c;  // lut_c: code table entries (tq_device.h kLutMax), 0 = none
+  float maxv_c;
+  double inv_c;
 };
 
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream);

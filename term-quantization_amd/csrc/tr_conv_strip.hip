@@ -104,6 +104,7 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
     o[e] = y[e];
     if (a.relu) {
       y[e] = y[e] > 0.0f ? y[e] : 0.0f;
+      if (a.relu == 2) y[e] = y[e] < 6.0f ? y[e] : 6.0f;  // ReLU6
       o[e] = o[e] != o[e] ? o[e] : y[e];  // the stored value keeps a NaN (torch.relu)
     }
   }

@@ -21,6 +21,11 @@ namespace {
 __device__ __forceinline__ int sext24(int v) { return (v << 8) >> 8; }
 
 __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
+  if (a.lut_c) {
+    lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
+    __syncthreads();
+  }
   const int chunks = a.Cp / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
@@ -61,9 +66,51 @@ __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int c = c0 + i;
-    const double sh = (a.bias && c < a.C) ? (double)a.bias[c] : 0.0;
-    y[i] = (float)((double)acc[i] * a.scale + sh);
+    if (a.ch_scale) {  // folded BN (pad channels: 0)
+      y[i] = c < a.C ? (float)((double)acc[i] * a.ch_scale[c] + a.ch_shift[c]) : 0.0f;
+    } else {
+      const double sh = (a.bias && c < a.C) ? (double)a.bias[c] : 0.0;
+      y[i] = (float)((double)acc[i] * a.scale + sh);
+    }
   }
+  if (a.relu) {  // the stored value keeps a NaN (torch.relu / hardtanh); codes see 0
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o[i] = y[i];
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;
+      o[i] = o[i] != o[i] ? o[i] : y[i];
+    }
+    if (a.out) {
+      float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
+      if ((a.C & 7) == 0) {
+        *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + i < a.C) dst[i] = o[i];
+      }
+    }
+  }
+  if (a.codes) {  // next layer's codes of channels c0 .. c0 + 7 (cp_c == Cp: same channels)
+    uint32_t v[8];
+    if (a.lut_c) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = lut[relu_q(y[i], a.inv_c, a.maxv_c)];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = code_bits(tr_value_g1_inv(y[i], a.inv_c, a.maxv_c, a.k_c), a.fmt_c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (c0 + i >= a.C) v[i] = 0u;  // pad channels: zero codes
+    *reinterpret_cast<uint4*>(a.codes + p * a.cp_c + c0) =
+        make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                   v[6] | (v[7] << 16));
+  }
+  if (a.relu || !a.out) return;
   if (a.out_nhwc) {
     float* dst = a.out + p * a.C + c0;
     if ((a.C & 7) == 0) {
@@ -86,7 +133,7 @@ __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.N * a.Ho * a.Wo * (a.Cp / 8);
   if (n == 0) return hipSuccess;
-  dwconv_tp_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(a);
+  dwconv_tp_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, (size_t)a.lut_c * 2, stream>>>(a);
   return hipGetLastError();
 }
 

@@ -312,3 +312,157 @@ class FusedResNet(nn.Module):
         x = m.avgpool(x)
         x = torch.flatten(x, 1)
         return m.fc(x)
+
+
+# ---------------------------------------------------------------------------------------
+# MobileNet-V2 (torchvision topology, cnn_models/mobilenet.py): inverted-residual blocks
+#   expand 1x1 -> BN -> ReLU6 -> dw 3x3 -> BN -> ReLU6 -> project 1x1 -> BN (+ identity)
+# with every BN / ReLU6 / residual add and the next layer's activation TR in the producing
+# kernel's epilogue (term-pair convs: tq_conv2d_termpair_f16 relu = 2; depthwise:
+# tq_dwconv2d_termpair_fused), so between the stem and the classifier only the term-pair
+# kernels touch HBM -- fp32 tensors only where a residual or the pooling needs them.
+
+
+class _Codes(object):
+    """What a producing epilogue needs to know about a consuming TR layer."""
+
+    def __init__(self, layer, code_dtype, nonneg):
+        self.quant = (layer.input_quant.sf, layer.data_bits, layer.data_terms)
+        self.cp_in = layer.act_channels
+        self.code_dtype = code_dtype
+        self.nonneg = nonneg
+
+
+class _DwConv(object):
+    """A depthwise TRConv2dLayer (mode "depthwise") + its BN + ReLU6, for the fused kernel."""
+
+    def __init__(self, layer, bn):
+        if not isinstance(layer, tr_layer.TRConv2dLayer) or layer.mode != "depthwise":
+            raise ValueError("fused executor needs depthwise term-pair TRConv2dLayers")
+        if layer.input_quant.tracking:
+            raise ValueError("calibrate first: set_tr_tracking(model, False)")
+        c = layer.conv
+        if any(tq_ops.static_padding(c)):
+            raise ValueError("static-same padding is not fused here")
+        self.layer = layer
+        self.c = c.out_channels
+        self.kh, self.kw = c.kernel_size
+        self.stride, self.padding, self.dilation = c.stride, c.padding, c.dilation
+        self.bn = bn
+        self.scale, self.shift = _fold_bn(layer, bn)
+        self.consumer = _Codes(layer, torch.int16, False)
+
+    def out_hw(self, h, w):
+        return (tq_ops.conv_out_size(h, self.kh, self.stride[0], self.padding[0],
+                                     self.dilation[0]),
+                tq_ops.conv_out_size(w, self.kw, self.stride[1], self.padding[1],
+                                     self.dilation[1]))
+
+    def __call__(self, codes, nxt, out=False):
+        n, h, w, cp = codes.shape
+        ho, wo = self.out_hw(h, w)
+        dev = codes.device
+        y = (torch.empty((n, self.c, ho, wo), dtype=torch.float32, device=dev,
+                         memory_format=torch.channels_last) if out else None)
+        nc = torch.empty((n, ho, wo, nxt.cp_in), dtype=nxt.code_dtype, device=dev)
+        if nxt.cp_in != cp:
+            raise ValueError("depthwise output codes must have the input's channel padding")
+        w_codes = self.layer.w_codes
+        nbytes = codes.numel() * 2 + nc.numel() * nc.element_size() + w_codes.numel() * 4 + \
+            (y.numel() * 4 if y is not None else 0)
+        tq_ops._launch(
+            "dwconv2d_termpair", n * ho * wo * self.c * self.kh * self.kw,
+            lambda: tq_native.dwconv2d_termpair_fused(
+                codes, self.c, w_codes, self.kh, self.kw, self.stride, self.padding,
+                self.dilation, ho, wo, self.scale, self.shift, 6, out=y, next_codes=nc,
+                quant=nxt.quant), nbytes)
+        return y, nc
+
+
+class _InvRes(object):
+    def __init__(self, block):
+        mods = list(block.conv)
+        self.use_res = block.use_res_connect
+        if len(mods) == 3:  # expand ratio 1: dw, project conv, BN
+            self.expand = None
+            dw, proj, bn = mods[0], mods[1], mods[2]
+        else:
+            self.expand = _Conv(mods[0][0], mods[0][1], nonneg=False)
+            dw, proj, bn = mods[1], mods[2], mods[3]
+        self.dw = _DwConv(dw[0], dw[1])
+        # the project conv's input codes are TR of a ReLU6 output: non-negative windows
+        self.project = _Conv(proj, bn, nonneg=True)
+
+    def first_consumer(self):
+        """The consumer of this block's input codes: the expand conv, else the dw conv."""
+        return self.expand if self.expand is not None else self.dw.consumer
+
+
+class FusedMobileNetV2(nn.Module):
+    """Inference executor over a converted + calibrated MobileNet-V2 (cnn_models.mobilenet_v2
+    with depthwise layers at (16, 1, 16) and the rest term-pair, cnn_models/__init__.py:31-58).
+    The stem conv (never converted: an fp32 torch conv, cnn_models/__init__.py:34-36) and the
+    classifier stay torch."""
+
+    def __init__(self, qmodel):
+        super(FusedMobileNetV2, self).__init__()
+        from cnn_models.mobilenet import InvertedResidual
+        self.qmodel = qmodel
+        feats = list(qmodel.features)
+        self.stem = feats[0]
+        self.blocks = [_InvRes(b) for b in feats[1:-1]]
+        if not all(isinstance(b, InvertedResidual) for b in feats[1:-1]):
+            raise ValueError("not a torchvision-style MobileNet-V2")
+        last = feats[-1]
+        self.last = _Conv(last[0], last[1], nonneg=False)
+
+    @torch.no_grad()
+    def forward(self, x, capture=None):
+        """Logits of a batch.  ``capture`` (a list, tests only) receives one record per
+        term-pair / depthwise layer: {"name", "kind", "conv", "codes_in", "residual", "out",
+        "codes_out"}; capture mode also stores every fp32 output."""
+        m = self.qmodel
+        keep = capture is not None
+        x = x.contiguous(memory_format=torch.channels_last)
+        y0 = self.stem(x).contiguous(memory_format=torch.channels_last)  # conv, BN, ReLU6
+        first = self.blocks[0].first_consumer()
+        codes = torch.empty((y0.shape[0], y0.shape[2], y0.shape[3], first.cp_in),
+                            dtype=first.code_dtype, device=x.device)
+        tq_ops._launch("act_encode", 4 * y0.numel() + 2 * codes.numel(),
+                       lambda: tq_native.act_encode(y0, True, *first.quant, codes))
+        xin = y0
+        for i, b in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            c_in = codes
+            if b.expand is not None:
+                h, hcodes, _ = b.expand(codes, out=True if keep else None, relu=6,
+                                        next_a=b.dw.consumer)
+                if keep:
+                    capture.append({"name": "block%d.expand" % i, "kind": "conv",
+                                    "conv": b.expand, "codes_in": codes, "residual": None,
+                                    "out": h, "codes_out": hcodes, "relu": 6})
+            else:
+                hcodes = codes
+            d, pcodes = b.dw(hcodes, b.project, out=keep)
+            if keep:
+                capture.append({"name": "block%d.dw" % i, "kind": "dw", "conv": b.dw,
+                                "codes_in": hcodes, "residual": None, "out": d,
+                                "codes_out": pcodes, "relu": 6})
+            consumer = nxt.first_consumer() if nxt is not None else self.last
+            need_out = keep or (nxt is not None and nxt.use_res)
+            xout, codes, _ = b.project(pcodes, out=True if need_out else None,
+                                       residual=xin if b.use_res else None, relu=False,
+                                       next_a=consumer)
+            if keep:
+                capture.append({"name": "block%d.project" % i, "kind": "conv",
+                                "conv": b.project, "codes_in": pcodes,
+                                "residual": xin if b.use_res else None, "out": xout,
+                                "codes_out": codes, "relu": 0})
+            xin = xout
+        y, _, _ = self.last(codes, out=True, relu=6)
+        if keep:
+            capture.append({"name": "last", "kind": "conv", "conv": self.last,
+                            "codes_in": codes, "residual": None, "out": y, "codes_out": None,
+                            "relu": 6})
+        y = nn.functional.adaptive_avg_pool2d(y, 1).reshape(y.shape[0], -1)
+        return m.classifier(y)

@@ -78,6 +78,16 @@ _SIGNATURES["tq_conv2d_termpair_fused"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
     _i64, _f64, _vp, _vp, _i64, _i64, ctypes.POINTER(ConvEpilogue), _vp]
 
+class DwEpilogue(ctypes.Structure):
+    """tq_dw_epilogue (include/tq.h)."""
+    _fields_ = [("ch_scale", _vp), ("ch_shift", _vp), ("relu", _i32), ("codes", _vp),
+                ("cp", _i64), ("sf", _f32), ("bits", _i32), ("terms", _i32), ("fmt", _i32)]
+
+
+_SIGNATURES["tq_dwconv2d_termpair_fused"] = [
+    _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+    _vp, _i64, _i64, ctypes.POINTER(DwEpilogue), _vp]
+
 _SIGNATURES["tq_stem_conv_pool_encode"] = [
     _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _i32,
     _vp, _i64, _f32, _i32, _i32, _i32, _vp]
@@ -343,7 +353,7 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
         raise RuntimeError("activation and weight codes must have the same format")
     epi = ConvEpilogue()
     epi.ch_scale, epi.ch_shift = _ptr(ch_scale), _ptr(ch_shift)
-    epi.residual, epi.relu = _ptr(residual), int(bool(relu))
+    epi.residual, epi.relu = _ptr(residual), (2 if relu == 6 else int(bool(relu)))
     if codes_a is not None:
         epi.codes_a, epi.cp_a = _ptr(codes_a), codes_a.shape[-1]
         epi.sf_a, epi.bits_a, epi.terms_a = float(quant_a[0]), int(quant_a[1]), int(quant_a[2])
@@ -388,6 +398,27 @@ def dwconv2d_termpair(codes, c, w_codes, kh, kw, stride, pad_tl, dilation, scale
                                         stride[0], stride[1], pad_tl[0], pad_tl[1],
                                         dilation[0], dilation[1], float(scale), _ptr(bias),
                                         _ptr(out), ho, wo, int(out_nhwc), _stream(codes))
+    _check(rc)
+    return out
+
+
+def dwconv2d_termpair_fused(codes, c, w_codes, kh, kw, stride, pad_tl, dilation, ho, wo,
+                            ch_scale, ch_shift, relu, out=None, next_codes=None, quant=None):
+    """Depthwise term-pair conv with the fused BN / ReLU(6) / next-layer-codes epilogue
+    (tq_dwconv2d_termpair_fused), channels_last; relu 0, 1 or 6."""
+    n, h, w, cp = codes.shape
+    epi = DwEpilogue()
+    epi.ch_scale, epi.ch_shift = _ptr(ch_scale), _ptr(ch_shift)
+    epi.relu = 2 if relu == 6 else int(bool(relu))
+    if next_codes is not None:
+        epi.codes, epi.cp = _ptr(next_codes), next_codes.shape[-1]
+        epi.sf, epi.bits, epi.terms = float(quant[0]), int(quant[1]), int(quant[2])
+        epi.fmt = code_format(next_codes)
+    with torch.cuda.device(codes.device):
+        rc = lib().tq_dwconv2d_termpair_fused(
+            _ptr(codes), n, h, w, c, cp, _ptr(w_codes), kh, kw, stride[0], stride[1],
+            pad_tl[0], pad_tl[1], dilation[0], dilation[1], _ptr(out), ho, wo,
+            ctypes.byref(epi), _stream(codes))
     _check(rc)
     return out
 

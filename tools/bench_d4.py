@@ -11,7 +11,9 @@
 * MobileNet-V2 / EfficientNet-b0 TQ (depthwise layers at wb=16, g=1, k=16 as
   cnn_models.static_conv_layer_settings sets them; other layers g=8, k=12, wb=db=9, dt=3),
   synthetic N(0,1) 256x3x224x224, random-init weights: images/s of the converted module path
-  (term-pair and depthwise term-pair kernels, torch BN/activations).
+  (term-pair and depthwise term-pair kernels, torch BN/activations), and for MobileNet-V2
+  also of the fused executor (tq_fuse.FusedMobileNetV2: BN / ReLU6 / residual / next-layer
+  TR in the kernels' epilogues).
 Timing: W untimed warmup steps, then K steps between synchronize calls."""
 import argparse
 import json
@@ -28,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
 import cnn_models  # noqa: E402
 import evaluate_lstm  # noqa: E402
 import profile_model  # noqa: E402
+import tq_fuse  # noqa: E402
 import tq_ops  # noqa: E402
 import tr_layer  # noqa: E402
 from lstm_models import model as model_mod  # noqa: E402
@@ -148,6 +151,13 @@ def cnn(arch, args, dev):
         tr_layer.set_tr_tracking(q, False)
         t = timed(lambda: q(x), args.steps, args.warmup)
         kernels = kernel_breakdown(lambda: q(x), args.steps, t)
+        fused = None
+        if arch == "mobilenet_v2":  # the fused inverted-residual executor (tq_fuse.py)
+            ex = tq_fuse.FusedMobileNetV2(q)
+            tf = timed(lambda: ex(x), args.steps, args.warmup)
+            fused = {"images_per_s": args.batch / tf, "ms_per_step": tf * 1e3,
+                     "term_pair_macs_per_s": tmacs * args.batch / tf,
+                     "kernels": kernel_breakdown(lambda: ex(x), args.steps, tf)}
     modes = sorted({m.mode for m in q.modules() if isinstance(m, tr_layer.TRConv2dLayer)})
     return {"metric": "%s TQ images/s" % arch, "value": args.batch / t, "unit": "images/s",
             "ms_per_step": t * 1e3, "term_pair_macs_per_image": tmacs,
@@ -155,7 +165,7 @@ def cnn(arch, args, dev):
             "config": {"workload": "%s-tq (dw wb=16 g=1 k=16; others g=8 k=12 wb=db=9 dt=3)"
                                    % arch, "batch": args.batch, "layer_modes": modes,
                        "data": "synthetic N(0,1), random-init weights"},
-            "kernels": kernels}
+            "kernels": kernels, "fused_executor": fused}
 
 
 def main():
