@@ -270,15 +270,58 @@ class FusedResNet(nn.Module):
         term-pair conv -- {"name", "conv", "codes_in", "residual", "out", "codes_a",
         "codes_b"} -- plus a "stem" record, and makes every conv also store its fp32 output
         (the epilogue computes it either way; the codes are identical)."""
+        res = []
+        for _ in self._steps(x, capture, res):
+            pass
+        return res[0]
+
+    @torch.no_grad()
+    def forward_streams(self, x, streams):
+        """Logits of a batch split into len(streams) image chunks, one chunk per HIP stream.
+        Each chunk runs the same kernels as forward() on its images (every kernel is
+        per-image independent, so the logits are bit-identical); the launches are issued
+        layer by layer, round-robin over the streams, so while one chunk's kernel drains
+        its last workgroups the other chunk's kernel fills the idle CUs."""
+        if len(streams) <= 1:
+            return self.forward(x)
+        cur = torch.cuda.current_stream(x.device)
+        chunks = x.chunk(len(streams))
+        gens, res = [], []
+        for s, xc in zip(streams, chunks):
+            s.wait_stream(cur)
+            r = []
+            res.append(r)
+            gens.append(self._steps(xc, None, r))
+        live = list(range(len(gens)))
+        while live:
+            nxt = []
+            for j in live:
+                with torch.cuda.stream(streams[j]):
+                    if next(gens[j], StopIteration) is not StopIteration:
+                        nxt.append(j)
+            live = nxt
+        capturing = torch.cuda.is_current_stream_capturing()
+        for s, xc, r in zip(streams, chunks, res):
+            cur.wait_stream(s)
+            if not capturing:  # (a captured graph keeps its private pool alive)
+                xc.record_stream(s)
+                r[0].record_stream(cur)
+        return torch.cat([r[0] for r in res])
+
+    def _steps(self, x, capture, result):
+        """forward() as a generator: yields after each kernel launch; the logits end up in
+        result[0]."""
         m = self.qmodel
         keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
         x, codes, codes_down = self._stem(x)
+        yield
         if keep:
             capture.append({"name": "stem", "out": x, "codes_a": codes, "codes_b": codes_down})
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             y1, mid, _ = b.conv1(codes, out=True if keep else None, relu=True, next_a=b.conv2)
+            yield
             if keep:
                 capture.append({"name": "block%d.conv1" % i, "conv": b.conv1, "codes_in": codes,
                                 "residual": None, "out": y1, "codes_a": mid, "codes_b": None})
@@ -286,6 +329,7 @@ class FusedResNet(nn.Module):
             if b.down is not None and (not fuse_ds or keep):
                 # (capture runs it separately as well, to record the identity it must equal)
                 identity, _, _ = b.down(codes_down, out=True)
+                yield
                 if keep:
                     capture.append({"name": "block%d.downsample" % i, "conv": b.down,
                                     "codes_in": codes_down, "residual": None, "out": identity,
@@ -303,6 +347,7 @@ class FusedResNet(nn.Module):
                 relu=True, next_a=nxt.conv1 if nxt else None,
                 next_b=None if shared else next_b,
                 downsample=(b.down, codes_down) if fuse_ds else None)
+            yield
             if shared:
                 codes_down = codes
             if keep:
@@ -311,7 +356,7 @@ class FusedResNet(nn.Module):
                                 "codes_b": codes_down})
         x = m.avgpool(x)
         x = torch.flatten(x, 1)
-        return m.fc(x)
+        result.append(m.fc(x))
 
 
 # ---------------------------------------------------------------------------------------

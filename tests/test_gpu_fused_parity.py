@@ -136,6 +136,21 @@ def test_fused_executor_teacher_forced_at_bench_config(bench_model):
             block_out = r["out"]
 
 
+@pytest.mark.parametrize("nstreams", [2, 4])
+def test_stream_split_is_bit_identical(bench_model, nstreams):
+    """forward_streams (bench.py --streams): the batch in image chunks on concurrent HIP
+    streams gives exactly forward()'s logits."""
+    qmodel, x = bench_model
+    fused = tq_fuse.FusedResNet(qmodel)
+    streams = [torch.cuda.Stream(DEV) for _ in range(nstreams)]
+    with torch.no_grad():
+        ref = fused(x)
+        for _ in range(2):
+            got = fused.forward_streams(x, streams)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got)
+
+
 def _quantize(y, quant):
     """q of kernels/tr_cuda_kernel.cu:21-23 for fp32 values y >= 0 (numpy)."""
     sf, db, _ = quant

@@ -40,6 +40,26 @@ def pmc(path, counter):
     return per
 
 
+def busy_us(trace_csv, needles):
+    """Union of the launch intervals of the matching kernels (us): the GPU time during which
+    at least one of them runs; equals the summed durations when launches do not overlap
+    (one stream) and is shorter when bench.py's chunk streams overlap them."""
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                for r in csv.DictReader(open(trace_csv))
+                if any(nd in r["Kernel_Name"] for nd in needles))
+    busy, cs, ce = 0, None, None
+    for s, e in iv:
+        if ce is None or s > ce:
+            if ce is not None:
+                busy += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    if ce is not None:
+        busy += ce - cs
+    return busy / 1e3
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
@@ -59,6 +79,9 @@ def main(tag):
         f = [v for n in fetch if any(nd in n for nd in needles) for v in fetch[n]]
         w = [v for n in write if any(nd in n for nd in needles) for v in write[n]]
         entry = {"variants": names, "calls": calls, "avg_duration_us": total_ns / calls / 1e3}
+        trace_csv = os.path.join(src, "kt", "kt_kernel_trace.csv")
+        if os.path.exists(trace_csv):
+            entry["busy_us_per_launch"] = busy_us(trace_csv, needles) / calls
         if f and w:
             entry["fetch_bytes_per_launch"] = 2.0 * sum(f) / len(f) * 1024
             entry["write_bytes_per_launch"] = sum(w) / len(w) * 1024
