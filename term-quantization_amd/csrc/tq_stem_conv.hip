@@ -30,15 +30,19 @@
 //        the input tile pre-split into two fp16 planes x0 = RN16(x), x1 = RN16(x - x0) of
 //        s2d rows [2TP+4][SC][12] each (the split of a value is done once, when its tile is
 //        staged, not per fragment read: every value feeds up to 16 taps x 4 Cout blocks)
-//   wave = one strip of 16 conv columns (7 pool columns) x 2TP+1 conv rows, two rows at a
+//   wave = one strip of 16 conv columns (7 pool columns) x 2TP+1 conv rows, four rows at a
 //        time; per row 6 K-steps x (4 Cout blocks x 3 split products)
-//        v_mfma_f32_16x16x32_f16, each weight fragment read once for both rows
-//   epilogue: BN (fp32 fma, as the stem-tail kernel) + ReLU, vertical max over the 3 conv
-//        rows of each pool row in registers, horizontal max by lane shuffles (width 16), the
-//        strip's 7 pool pixels x 64 channels compacted through LDS (1.8 KB per wave), then
-//        contiguous fp32 stores + TR codes, every lane finishing 4 channels of <= 2 quads.
-// Max-pool pads with -inf; after ReLU every window holds a valid value >= 0, so the padded
-// conv positions are read as 0 here with the same result.
+//        v_mfma_f32_16x16x32_f16, each weight fragment read once for the four rows (the
+//        kernel is bound by LDS fragment reads: two-row passes read the weights twice as
+//        often)
+//   epilogue: vertical max over the 3 conv rows of each pool row in registers, horizontal
+//        max by lane shuffles (width 16), the strip's 7 pool pixels x 64 channels compacted
+//        through LDS (1.8 KB per wave), then BN (fp32 fma, as the stem-tail kernel) + ReLU
+//        of each pooled value, contiguous fp32 stores + TR codes, every lane finishing 4
+//        channels of <= 2 quads.  Pooling the raw sums first is exact: the weights of
+//        channels with a negative BN scale are negated when staged, so BN (with |scale|) and
+//        ReLU are non-decreasing in the pooled value and commute with max.  Conv positions in
+//        the pool's padding are -inf, as in torch's max-pool.
 #include <type_traits>
 
 #include "tq_device.h"
@@ -96,22 +100,23 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   const int Hc = a.H / 2, Wc = a.W / 2;  // conv output
   const int tpi = (a.Ho + TP - 1) / TP;  // tiles per image
 
-  // weights once per workgroup: [2][64][192] fp16 -> rows of kStemWRow
+  // weights once per workgroup: [2][64][192] fp16 -> rows of kStemWRow, each output channel's
+  // row negated where its BN scale is negative (exact), so that every channel's BN is
+  // non-decreasing in its (sign-adjusted) conv sum and the max-pool can run before BN
   for (int i = tid; i < 2 * 64 * (kStemK / 8); i += kStemThreads) {
     const int row = i / (kStemK / 8);
     const int ch = i - row * (kStemK / 8);
-    *reinterpret_cast<u32x4*>(ws + row * kStemWRow + ch * 8) =
-        *reinterpret_cast<const u32x4*>(a.wsplit + row * kStemK + ch * 8);
+    u32x4 v = *reinterpret_cast<const u32x4*>(a.wsplit + row * kStemK + ch * 8);
+    if (__builtin_signbit(a.scale[row & 63])) v ^= (u32x4)0x80008000u;
+    *reinterpret_cast<u32x4*>(ws + row * kStemWRow + ch * 8) = v;
   }
-  // per-lane BN coefficients of channels mb*16 + 4g + i
-  float bsc[4][4], bsh[4][4];
+  // BN coefficients (|scale|, shift) of the channels 4 (lane % 16) .. +3 this lane finishes
+  float bsc[4], bsh[4];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bsc[mb][i] = a.scale[mb * 16 + 4 * g + i];
-      bsh[mb][i] = a.shift[mb * 16 + 4 * g + i];
-    }
+  for (int i = 0; i < 4; ++i) {
+    bsc[i] = fabsf(a.scale[4 * i16 + i]);
+    bsh[i] = a.shift[4 * i16 + i];
+  }
 
   // Input staging, software-pipelined across tiles: the next tile's rows are loaded into
   // registers while this tile computes, and written to LDS between the two.  Wave w moves
@@ -240,22 +245,20 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         h0 = __builtin_shufflevector(a0, b0, 0, 1, 2, 3, 4, 5, 6, 7);
         h1 = __builtin_shufflevector(a1, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       };
-      auto conv_rows = [&](auto nr_tag, int rr, f32x4 (&y)[2][4]) {
+      auto conv_rows = [&](auto nr_tag, int rr, f32x4 (&y)[4][4]) {
         constexpr int NR = decltype(nr_tag)::value;
         f32x4 acc[NR][4];
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) acc[r][mb] = (f32x4)0.0f;
-        f16x8 x0[NR], x1[NR], n0[NR], n1[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) load_x(rr + r, 0, x0[r], x1[r]);
 #pragma unroll 1
         for (int ks = 0; ks < kStemK / 32; ++ks) {
-          if (ks + 1 < kStemK / 32) {
+          // (no register double buffer of the input slices: with four rows in flight their
+          // loads' latency hides behind the other rows' MFMAs, and the registers are full)
+          f16x8 x0[NR], x1[NR];
 #pragma unroll
-            for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 1, n0[r], n1[r]);
-          }
+          for (int r = 0; r < NR; ++r) load_x(rr + r, ks, x0[r], x1[r]);
           {
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) {
@@ -272,12 +275,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             }
           }
           }
-#pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            x0[r] = n0[r];
-            x1[r] = n1[r];
-          }
         }
+        // raw (sign-adjusted) sums; conv positions outside the image pool as -inf
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
           const int oy = 2 * py0 - 1 + rr + r;
@@ -285,10 +284,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float v = fmaf(ldexpf(acc[r][mb][i], kback), bsc[mb][i], bsh[mb][i]);
-              y[r][mb][i] = ok ? fmaxf(v, 0.0f) : 0.0f;
-            }
+            for (int i = 0; i < 4; ++i) y[r][mb][i] = ok ? acc[r][mb][i] : -__builtin_inff();
         }
       };
 
@@ -328,7 +324,12 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           const int co = 4 * (f & 15);
           const int64_t p = p0 + (f >> 4);
           const f32x4 v4 = *reinterpret_cast<const f32x4*>(pb + 4 * f);
-          const float yv[4] = {v4[0], v4[1], v4[2], v4[3]};
+          // BN + ReLU of the pooled sum: both are non-decreasing in it (scale >= 0 after the
+          // weight sign flip, fp32 rounding is monotone), so relu(bn(max)) == max(relu(bn))
+          // bit for bit -- one BN per pool output instead of one per conv output
+          float yv[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) yv[i] = fmaxf(fmaf(ldexpf(v4[i], kback), bsc[i], bsh[i]), 0.0f);
           *reinterpret_cast<float4*>(a.out + p * 64 + co) =
               make_float4(yv[0], yv[1], yv[2], yv[3]);
 #pragma unroll
@@ -362,14 +363,21 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         __builtin_amdgcn_wave_barrier();  // pb is rewritten by the next pool row
       };
 
+      // conv rows in passes of four (4p .. 4p+3), every weight fragment read once per pass:
+      // pass p closes pool row 2p-1 (rows 4p-2, 4p-1 carried in run, and 4p) and pool row 2p
+      // (rows 4p .. 4p+2), and carries rows 4p+2, 4p+3; the last conv row 2TP closes pool
+      // row TP-1.
       f32x4 run[4];
-      f32x4 y[2][4];
+      f32x4 y[4][4];
 #pragma unroll 1
-      for (int i = 0; i < TP; ++i) {
-        conv_rows(std::integral_constant<int, 2>(), 2 * i, y);
-        if (i > 0) emit_pool(i - 1, run, y[0]);
+      for (int p = 0; p < TP / 2; ++p) {
+        conv_rows(std::integral_constant<int, 4>(), 4 * p, y);
+        if (p > 0) emit_pool(2 * p - 1, run, y[0]);
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[0][mb], y[1][mb]);
+        emit_pool(2 * p, run, y[2]);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[2][mb], y[3][mb]);
       }
       conv_rows(std::integral_constant<int, 1>(), 2 * TP, y);
       emit_pool(TP - 1, run, y[0]);
