@@ -164,6 +164,29 @@ __device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
   return (uint32_t)r + (__builtin_amdgcn_fractf(r) >= 0.5f ? 1u : 0u);
 }
 
+// Fused-epilogue activation (ConvArgs / DwConvArgs relu): 0 none, 1 ReLU, 2 ReLU6 (MobileNet-V2),
+// 3 swish y * sigmoid(y) (EfficientNet's MemoryEfficientSwish, with torch's fp32 sigmoid
+// 1 / (1 + exp(-y))).  y becomes the value the next layer's codes encode, o the stored value:
+// ReLU / ReLU6 keep a NaN in the stored value as torch.relu does (its codes are 0 either way:
+// TR(NaN) = 0).
+constexpr int kActSwish = 3;
+
+__device__ __forceinline__ void act_apply(int act, float& y, float& o) {
+  o = y;
+  if (act == kActSwish) {
+    y = y * (1.0f / (1.0f + expf(-y)));
+    o = y;
+  } else if (act) {
+    y = y > 0.0f ? y : 0.0f;
+    if (act == 2) y = y < 6.0f ? y : 6.0f;
+    o = o != o ? o : y;
+  }
+}
+
+// True when the activation leaves y >= 0 and never NaN, so the next layer's codes may take
+// the ReLU fast path and the code tables.
+__host__ __device__ inline bool act_nonneg(int act) { return act == 1 || act == 2; }
+
 // Activation / weight code formats of the term-pair kernels (include/tq.h TQ_CODES_*):
 // the same signed integer term sum v stored as int16 (VALU dot2 engine) or as the fp16
 // value v (MFMA engine; exact for |v| <= 2048, i.e. bitwidth <= 11).

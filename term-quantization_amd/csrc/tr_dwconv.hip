@@ -73,15 +73,10 @@ __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
       y[i] = (float)((double)acc[i] * a.scale + sh);
     }
   }
-  if (a.relu) {  // the stored value keeps a NaN (torch.relu / hardtanh); codes see 0
+  if (a.relu) {  // ReLU / ReLU6 / swish; the stored value keeps a NaN (torch.relu / hardtanh)
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      o[i] = y[i];
-      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
-      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;
-      o[i] = o[i] != o[i] ? o[i] : y[i];
-    }
+    for (int i = 0; i < 8; ++i) act_apply(a.relu, y[i], o[i]);
     if (a.out) {
       float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
       if ((a.C & 7) == 0) {

@@ -96,7 +96,7 @@ class _Conv(object):
         """``downsample`` = (_Conv, its input codes): computed in this launch as a second
         accumulation phase, its identity added in place of ``residual``."""
         for nxt in (next_a, next_b):
-            if nxt is not None and nxt.nonneg and not relu:
+            if nxt is not None and nxt.nonneg and not (relu is True or relu in (1, 6)):
                 raise ValueError("a consumer with non-negative windows needs ReLU'd codes")
         n, h, w, _ = codes.shape
         ho, wo = self.out_hw(h, w)
@@ -387,8 +387,9 @@ class _DwConv(object):
         if layer.input_quant.tracking:
             raise ValueError("calibrate first: set_tr_tracking(model, False)")
         c = layer.conv
-        if any(tq_ops.static_padding(c)):
-            raise ValueError("static-same padding is not fused here")
+        # Conv2dStaticSamePadding (EfficientNet): taps outside the input read 0, so the
+        # (top, left) pad plus the padded output size express the asymmetric padding
+        self.pad_tblr = tq_ops.static_padding(c)
         self.layer = layer
         self.c = c.out_channels
         self.kh, self.kw = c.kernel_size
@@ -398,29 +399,35 @@ class _DwConv(object):
         self.consumer = _Codes(layer, torch.int16, False)
 
     def out_hw(self, h, w):
-        return (tq_ops.conv_out_size(h, self.kh, self.stride[0], self.padding[0],
-                                     self.dilation[0]),
-                tq_ops.conv_out_size(w, self.kw, self.stride[1], self.padding[1],
-                                     self.dilation[1]))
+        top, bottom, left, right = self.pad_tblr
+        return (tq_ops.conv_out_size(h + top + bottom, self.kh, self.stride[0],
+                                     self.padding[0], self.dilation[0]),
+                tq_ops.conv_out_size(w + left + right, self.kw, self.stride[1],
+                                     self.padding[1], self.dilation[1]))
 
-    def __call__(self, codes, nxt, out=False):
+    def __call__(self, codes, nxt, out=False, act=6):
+        """BN + ``act`` (6: ReLU6, "swish") in the epilogue; ``nxt`` (a _Codes / _Conv) gets
+        its input codes unless None (then ``out`` must be set)."""
         n, h, w, cp = codes.shape
         ho, wo = self.out_hw(h, w)
         dev = codes.device
         y = (torch.empty((n, self.c, ho, wo), dtype=torch.float32, device=dev,
                          memory_format=torch.channels_last) if out else None)
-        nc = torch.empty((n, ho, wo, nxt.cp_in), dtype=nxt.code_dtype, device=dev)
-        if nxt.cp_in != cp:
-            raise ValueError("depthwise output codes must have the input's channel padding")
+        nc = None
+        if nxt is not None:
+            nc = torch.empty((n, ho, wo, nxt.cp_in), dtype=nxt.code_dtype, device=dev)
+            if nxt.cp_in != cp:
+                raise ValueError("depthwise output codes must have the input's channel padding")
         w_codes = self.layer.w_codes
-        nbytes = codes.numel() * 2 + nc.numel() * nc.element_size() + w_codes.numel() * 4 + \
-            (y.numel() * 4 if y is not None else 0)
+        nbytes = codes.numel() * 2 + w_codes.numel() * 4 + \
+            sum(t.numel() * t.element_size() for t in (y, nc) if t is not None)
+        pad_tl = (self.pad_tblr[0] + self.padding[0], self.pad_tblr[2] + self.padding[1])
         tq_ops._launch(
             "dwconv2d_termpair", n * ho * wo * self.c * self.kh * self.kw,
             lambda: tq_native.dwconv2d_termpair_fused(
-                codes, self.c, w_codes, self.kh, self.kw, self.stride, self.padding,
-                self.dilation, ho, wo, self.scale, self.shift, 6, out=y, next_codes=nc,
-                quant=nxt.quant), nbytes)
+                codes, self.c, w_codes, self.kh, self.kw, self.stride, pad_tl,
+                self.dilation, ho, wo, self.scale, self.shift, act, out=y, next_codes=nc,
+                quant=nxt.quant if nxt is not None else None), nbytes)
         return y, nc
 
 
@@ -511,3 +518,130 @@ class FusedMobileNetV2(nn.Module):
                             "relu": 6})
         y = nn.functional.adaptive_avg_pool2d(y, 1).reshape(y.shape[0], -1)
         return m.classifier(y)
+
+
+# ---------------------------------------------------------------------------------------
+# EfficientNet-b0 (efficientnet_pytorch topology, cnn_models/efficientnet.py): MBConv blocks
+#   [expand 1x1 -> BN -> swish] -> dw kxk (static same padding) -> BN -> swish
+#   -> squeeze-excite: x * sigmoid(se_expand(swish(se_reduce(avgpool(x)))))
+#   -> project 1x1 -> BN (+ identity)
+# The expand conv's epilogue applies BN + swish and writes the dw conv's codes; the dw
+# kernel applies BN + swish and writes the fp32 tensor the squeeze-excite branch pools; the
+# gate and the project conv's input TR are one pass (tq_act_encode_gated); the project
+# conv's epilogue adds BN and the identity and writes the next block's codes.  The squeeze-
+# excite convs themselves (1x1 on [N, C, 1, 1], 16-bit weights: the module's term-pair
+# "wide" kernel) and the pooling stay module calls: a few KB per image.
+
+
+def _conv_out_static(conv, h, w):
+    top, bottom, left, right = tq_ops.static_padding(conv.conv)
+    c = conv.conv
+    return (tq_ops.conv_out_size(h + top + bottom, c.kernel_size[0], c.stride[0], c.padding[0],
+                                 c.dilation[0]),
+            tq_ops.conv_out_size(w + left + right, c.kernel_size[1], c.stride[1], c.padding[1],
+                                 c.dilation[1]))
+
+
+class _MBConv(object):
+    def __init__(self, block):
+        self.block = block
+        self.expand = None
+        for conv in (getattr(block, "_expand_conv", None), block._project_conv):
+            if conv is not None and any(tq_ops.static_padding(conv.conv)):
+                raise ValueError("1x1 convs of an MBConv block have no padding")
+        if block.expand_ratio != 1:
+            # its input is a block output (no activation): general exactness windows
+            self.expand = _Conv(block._expand_conv, block._bn0, nonneg=False)
+        self.dw = _DwConv(block._depthwise_conv, block._bn1)
+        self.has_se = block.has_se
+        # the project conv's input is swish(...) * gate: signed, general windows
+        self.project = _Conv(block._project_conv, block._bn2, nonneg=False)
+        self.use_res = (block.id_skip and block.stride == 1 and
+                        block.input_filters == block.output_filters)
+
+    def first_consumer(self):
+        return self.expand if self.expand is not None else self.dw.consumer
+
+    def gate(self, d):
+        """sigmoid(se_expand(swish(se_reduce(avgpool(d))))) as fp32 [N, C] (module calls:
+        the squeeze-excite convs are TRConv2dLayers, efficientnet_pytorch's composition)."""
+        b = self.block
+        x_sq = nn.functional.adaptive_avg_pool2d(d, 1)
+        x_sq = b._se_expand(b._swish(b._se_reduce(x_sq)))
+        return torch.sigmoid(x_sq).reshape(d.shape[0], d.shape[1]).contiguous()
+
+
+class FusedEfficientNet(nn.Module):
+    """Inference executor over a converted + calibrated EfficientNet-b0 (cnn_models.
+    efficientnet_b0 with depthwise and squeeze-excite convs at (16, 1, 16) and the rest
+    term-pair, cnn_models/__init__.py:31-58).  The stem conv (never converted) and the
+    classifier stay torch."""
+
+    def __init__(self, qmodel):
+        super(FusedEfficientNet, self).__init__()
+        from cnn_models.efficientnet import MBConvBlock
+        self.qmodel = qmodel
+        if not all(isinstance(b, MBConvBlock) for b in qmodel._blocks):
+            raise ValueError("not an efficientnet_pytorch-style EfficientNet")
+        self.blocks = [_MBConv(b) for b in qmodel._blocks]
+        self.head = _Conv(qmodel._conv_head, qmodel._bn1, nonneg=False)
+
+    @torch.no_grad()
+    def forward(self, x, capture=None):
+        """Logits of a batch.  ``capture`` (a list, tests only) receives one record per
+        term-pair / depthwise layer: {"name", "kind", "conv", "codes_in", "residual", "out",
+        "codes_out", "act", "gate"}; capture mode also stores every fp32 output."""
+        m = self.qmodel
+        keep = capture is not None
+        x = x.contiguous(memory_format=torch.channels_last)
+        y0 = m._swish(m._bn0(m._conv_stem(x))).contiguous(memory_format=torch.channels_last)
+        first = self.blocks[0].first_consumer()
+        codes = torch.empty((y0.shape[0], y0.shape[2], y0.shape[3], first.cp_in),
+                            dtype=first.code_dtype, device=x.device)
+        tq_ops._launch("act_encode", 4 * y0.numel() + 2 * codes.numel(),
+                       lambda: tq_native.act_encode(y0, True, *first.quant, codes))
+        xin = y0
+        for i, b in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            if b.expand is not None:
+                h, hcodes, _ = b.expand(codes, out=True if keep else None, relu="swish",
+                                        next_a=b.dw.consumer)
+                if keep:
+                    capture.append({"name": "block%d.expand" % i, "kind": "conv",
+                                    "conv": b.expand, "codes_in": codes, "residual": None,
+                                    "out": h, "codes_out": hcodes, "act": "swish"})
+            else:
+                hcodes = codes
+            if b.has_se:
+                d, _ = b.dw(hcodes, None, out=True, act="swish")
+                g = b.gate(d)
+                pcodes = torch.empty((d.shape[0], d.shape[2], d.shape[3], b.project.cp_in),
+                                     dtype=b.project.code_dtype, device=x.device)
+                tq_ops._launch("act_encode_gated", 4 * d.numel() + 2 * pcodes.numel(),
+                               lambda: tq_native.act_encode_gated(d, g, *b.project.quant,
+                                                                  pcodes))
+            else:
+                d, pcodes = b.dw(hcodes, b.project, out=keep, act="swish")
+                g = None
+            if keep:
+                capture.append({"name": "block%d.dw" % i, "kind": "dw", "conv": b.dw,
+                                "codes_in": hcodes, "residual": None, "out": d,
+                                "codes_out": pcodes, "act": "swish", "gate": g})
+            consumer = nxt.first_consumer() if nxt is not None else self.head
+            need_out = keep or (nxt is not None and nxt.use_res)
+            xout, codes, _ = b.project(pcodes, out=True if need_out else None,
+                                       residual=xin if b.use_res else None, relu=False,
+                                       next_a=consumer)
+            if keep:
+                capture.append({"name": "block%d.project" % i, "kind": "conv",
+                                "conv": b.project, "codes_in": pcodes,
+                                "residual": xin if b.use_res else None, "out": xout,
+                                "codes_out": codes, "act": None})
+            xin = xout
+        y, _, _ = self.head(codes, out=True, relu="swish")
+        if keep:
+            capture.append({"name": "head", "kind": "conv", "conv": self.head,
+                            "codes_in": codes, "residual": None, "out": y, "codes_out": None,
+                            "act": "swish"})
+        y = m._avg_pooling(y).flatten(start_dim=1)
+        return m._fc(m._dropout(y))

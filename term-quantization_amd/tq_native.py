@@ -39,6 +39,8 @@ _SIGNATURES = {
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
                          _vp],
+    "tq_act_encode_gated": [_vp, _i64, _i64, _i64, _i64, _vp, _f32, _i32, _i32, _vp, _i64,
+                            _i32, _vp],
     "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _i32,
                       _vp],
     "tq_conv2d_cout_align": [],
@@ -258,6 +260,31 @@ def act_encode(x, in_nhwc, sf, bitwidth, num_keep_terms, codes):
     return codes
 
 
+def act_code(relu):
+    """Epilogue activation code of include/tq.h: False/0 none, True/1 ReLU, 6 ReLU6,
+    "swish" swish (EfficientNet)."""
+    if relu == "swish":
+        return 3
+    return 2 if relu == 6 else int(bool(relu))
+
+
+def act_encode_gated(x, gate, sf, bitwidth, num_keep_terms, codes):
+    """codes = TR(gate[n, c] * x) (tq_act_encode_gated): x fp32 channels_last [N, C, H, W],
+    gate fp32 [N, C] -- EfficientNet's squeeze-excite scaling fused into the project conv's
+    input TR."""
+    n, c, h, w = x.shape
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("act_encode_gated: x must be channels_last")
+    if gate.dtype != torch.float32 or tuple(gate.shape) != (n, c) or not gate.is_contiguous():
+        raise RuntimeError("act_encode_gated: gate must be a contiguous fp32 [N, C] tensor")
+    with torch.cuda.device(x.device):
+        rc = lib().tq_act_encode_gated(_ptr(x), n, c, h, w, _ptr(gate), sf, bitwidth,
+                                       num_keep_terms, _ptr(codes), codes.shape[-1],
+                                       code_format(codes), _stream(x))
+    _check(rc)
+    return codes
+
+
 def conv2d_cout_align():
     return int(lib().tq_conv2d_cout_align())
 
@@ -353,7 +380,7 @@ def conv2d_termpair_fused(codes, w_codes, cout, kh, kw, stride, padding, dilatio
         raise RuntimeError("activation and weight codes must have the same format")
     epi = ConvEpilogue()
     epi.ch_scale, epi.ch_shift = _ptr(ch_scale), _ptr(ch_shift)
-    epi.residual, epi.relu = _ptr(residual), (2 if relu == 6 else int(bool(relu)))
+    epi.residual, epi.relu = _ptr(residual), act_code(relu)
     if codes_a is not None:
         epi.codes_a, epi.cp_a = _ptr(codes_a), codes_a.shape[-1]
         epi.sf_a, epi.bits_a, epi.terms_a = float(quant_a[0]), int(quant_a[1]), int(quant_a[2])
@@ -405,11 +432,11 @@ def dwconv2d_termpair(codes, c, w_codes, kh, kw, stride, pad_tl, dilation, scale
 def dwconv2d_termpair_fused(codes, c, w_codes, kh, kw, stride, pad_tl, dilation, ho, wo,
                             ch_scale, ch_shift, relu, out=None, next_codes=None, quant=None):
     """Depthwise term-pair conv with the fused BN / ReLU(6) / next-layer-codes epilogue
-    (tq_dwconv2d_termpair_fused), channels_last; relu 0, 1 or 6."""
+    (tq_dwconv2d_termpair_fused), channels_last; relu 0, 1, 6 or "swish"."""
     n, h, w, cp = codes.shape
     epi = DwEpilogue()
     epi.ch_scale, epi.ch_shift = _ptr(ch_scale), _ptr(ch_shift)
-    epi.relu = 2 if relu == 6 else int(bool(relu))
+    epi.relu = act_code(relu)
     if next_codes is not None:
         epi.codes, epi.cp = _ptr(next_codes), next_codes.shape[-1]
         epi.sf, epi.bits, epi.terms = float(quant[0]), int(quant[1]), int(quant[2])

@@ -1,0 +1,136 @@
+"""GPU parity of the fused EfficientNet-b0 executor (tq_fuse.FusedEfficientNet), teacher forced
+layer by layer as tests/test_gpu_fused_mbv2.py does for MobileNet-V2: for every term-pair and
+depthwise layer of a converted, calibrated EfficientNet-b0 (cnn_models/__init__.py:31-58:
+depthwise and squeeze-excite convs at (16, 1, 16), the rest g=8 k=12 wb=db=9 dt=3), on a
+sample of images,
+  (i)  its fp32 output is within 1e-5 (x 1.1, swish's Lipschitz bound) of the fp64
+       composition conv (static same padding) -> BN -> (swish | + identity) of the very
+       codes it consumed (tr_layer.py:124-126 + efficientnet_pytorch's MBConvBlock), and
+  (ii) the codes it emitted are bit-exact oracle.tr() of its stored fp32 output -- for the
+       depthwise layers, of fp32(gate * output) with the squeeze-excite gate (the project
+       conv's input, MBConvBlock.forward: x = sigmoid(x_sq) * x).
+The bench-mode logits are bit-identical to the capture-mode ones."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import cnn_models
+import oracle
+import tq_fuse
+import tq_ops
+import tr_layer
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SAMPLE = [0, 5]
+
+
+def _nchw(t, idx):
+    return t[idx].double().cpu().contiguous()
+
+
+def _codes(t, idx, c):
+    return t[idx][..., :c].double().permute(0, 3, 1, 2).cpu().contiguous()
+
+
+def _bn(bn, z):
+    a = bn.weight.detach().double().cpu() / torch.sqrt(bn.running_var.double().cpu() + bn.eps)
+    return ((z - bn.running_mean.double().cpu().view(1, -1, 1, 1)) * a.view(1, -1, 1, 1) +
+            bn.bias.detach().double().cpu().view(1, -1, 1, 1)), a
+
+
+def _tr_codes(y, quant):
+    sf, db, dt = quant
+    yq = oracle.tr(y.float().numpy().reshape(1, -1, 1, 1), sf, db, 1, dt)
+    return torch.from_numpy(np.rint(yq.reshape(y.shape) / np.float32(sf)).astype(np.int64))
+
+
+@pytest.fixture(scope="module")
+def net():
+    torch.manual_seed(0)
+    model = cnn_models.efficientnet_b0(pretrained=False).to(DEV).eval()
+    with torch.no_grad():  # non-trivial BN statistics
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 2.0)
+    st = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, st, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        q(x)
+    tr_layer.set_tr_tracking(q, False)
+    return q, x
+
+
+def _consumer_quant(cap, codes):
+    for cand in cap:
+        if cand["codes_in"] is codes:
+            cc = cand["conv"]
+            return cc.consumer.quant if cand["kind"] == "dw" else cc.quant
+    return None
+
+
+def test_fused_efficientnet_b0_teacher_forced(net):
+    q, x = net
+    fused = tq_fuse.FusedEfficientNet(q)
+    cap = []
+    logits_cap = fused(x, capture=cap)
+    logits = fused(x)
+    torch.cuda.synchronize()
+    assert torch.equal(logits, logits_cap)
+    assert len(cap) == 16 + 16 + 15 + 1  # dw + project per block, 15 expand convs, the head
+    for rec in cap:
+        conv = rec["conv"]
+        layer = conv.layer
+        sf = (conv.consumer.quant if rec["kind"] == "dw" else conv.quant)[0]
+        c = layer.conv
+        c_in = c.in_channels
+        assert bool((rec["codes_in"][SAMPLE][..., c_in:] == 0).all()), rec["name"]
+        xq = _codes(rec["codes_in"], SAMPLE, c_in) * float(np.float32(sf))
+        top, bottom, left, right = tq_ops.static_padding(c)
+        xq = F.pad(xq, (left, right, top, bottom))
+        wq = c.weight.detach().double().cpu()
+        z = F.conv2d(xq, wq, None, c.stride, c.padding, c.dilation, c.groups)
+        mag = F.conv2d(xq.abs(), wq.abs(), None, c.stride, c.padding, c.dilation, c.groups)
+        ref, a = _bn(conv.bn, z)
+        bound_mag = mag * a.abs().view(1, -1, 1, 1)
+        if rec["residual"] is not None:
+            r = _nchw(rec["residual"], SAMPLE)
+            ref = ref + r
+            bound_mag = bound_mag + r.abs()
+        bound = 1e-5 * torch.maximum(ref.abs(), bound_mag)
+        if rec["act"] == "swish":
+            ref = ref * torch.sigmoid(ref)
+            bound = 1.1 * bound + 1e-6 * ref.abs()
+        y = _nchw(rec["out"], SAMPLE)
+        err = (y - ref).abs()
+        assert bool((err <= bound + 1e-30).all()), (rec["name"], float((err / bound).max()))
+        if rec["codes_out"] is None:
+            continue
+        quant = _consumer_quant(cap, rec["codes_out"])
+        assert quant is not None, rec["name"]
+        co = y.shape[1]
+        val = y
+        if rec.get("gate") is not None:  # fp32(gate * y), as the module's sigmoid(x_sq) * x
+            g = rec["gate"][SAMPLE].cpu().float().view(len(SAMPLE), co, 1, 1)
+            val = (g * y.float()).double()
+        got = _codes(rec["codes_out"], SAMPLE, co).long()
+        assert torch.equal(got, _tr_codes(val, quant)), rec["name"]
+
+
+def test_fused_efficientnet_b0_matches_module_path(net):
+    """Whole network against the module path (the reference composition): the logits agree
+    to the accumulated effect of midpoint code flips (a loose end-to-end sanity check; the
+    per-layer parity above is the bar)."""
+    q, x = net
+    fused = tq_fuse.FusedEfficientNet(q)
+    with torch.no_grad():
+        a = fused(x)
+        b = q(x)
+    torch.cuda.synchronize()
+    rel = ((a - b).norm() / b.norm()).item()
+    assert rel < 5e-2, rel

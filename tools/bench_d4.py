@@ -62,7 +62,7 @@ def kernel_breakdown(fn, steps, total_s):
             tf = 2 * k["work"] / k["seconds"] / 1e12
             e.update({"bound": "mfma", "achieved_tflops": tf, "peak_tflops": MFMA_F16_PEAK_TFLOPS,
                       "frac": tf / MFMA_F16_PEAK_TFLOPS})
-        elif name in ("act_encode",):
+        elif name in ("act_encode", "act_encode_gated"):
             gbs = k["work"] / k["seconds"] / 1e9
             e.update({"bound": "hbm", "achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
                       "frac": gbs / HBM_PEAK_GBS})
@@ -152,8 +152,9 @@ def cnn(arch, args, dev):
         t = timed(lambda: q(x), args.steps, args.warmup)
         kernels = kernel_breakdown(lambda: q(x), args.steps, t)
         fused = None
-        if arch == "mobilenet_v2":  # the fused inverted-residual executor (tq_fuse.py)
-            ex = tq_fuse.FusedMobileNetV2(q)
+        if arch in ("mobilenet_v2", "efficientnet_b0"):  # fused executors (tq_fuse.py)
+            ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
+                  tq_fuse.FusedEfficientNet)(q)
             tf = timed(lambda: ex(x), args.steps, args.warmup)
             fused = {"images_per_s": args.batch / tf, "ms_per_step": tf * 1e3,
                      "term_pair_macs_per_s": tmacs * args.batch / tf,
@@ -173,11 +174,17 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--only", choices=("lstm", "mobilenet_v2", "efficientnet_b0"),
+                    help="run one config")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = True
-    for fn in (lambda: lstm(args, dev), lambda: cnn("mobilenet_v2", args, dev),
-               lambda: cnn("efficientnet_b0", args, dev)):
+    runs = [("lstm", lambda: lstm(args, dev)),
+            ("mobilenet_v2", lambda: cnn("mobilenet_v2", args, dev)),
+            ("efficientnet_b0", lambda: cnn("efficientnet_b0", args, dev))]
+    for name, fn in runs:
+        if args.only and name != args.only:
+            continue
         r = fn()
         if not math.isfinite(r["value"]):
             raise RuntimeError("non-finite result")
