@@ -82,16 +82,20 @@ int tq_act_encode(const float *x, int32_t in_nhwc, int64_t n, int64_t c, int64_t
                   int64_t cp, int32_t fmt, void *stream);
 
 /*
- * Squeeze-excite gate + activation TR of EfficientNet-b0's MBConv blocks
- * (efficientnet_pytorch MBConvBlock.forward: x = torch.sigmoid(x_sq) * x, then the project
- * conv's input TR, tr_layer.py:96-99): codes[p][c] = TR(fp32(gate[img][c] * x[p][c])) with
- *   x     [n][h][w][c] fp32 (channels_last), 16-byte aligned
- *   gate  [n][c] fp32 (the sigmoid of the squeeze-excite branch), 16-byte aligned
- *   codes [n][h][w][cp] as tq_act_encode (pad channels 0); 0 < sf < inf.
+ * Activation / squeeze-excite gate + activation TR of EfficientNet-b0's MBConv tensors
+ * (efficientnet_pytorch MBConvBlock.forward: swish(bn0(expand_conv(x))), and
+ * x = torch.sigmoid(x_sq) * x before the project conv; the consumer's input TR,
+ * tr_layer.py:96-99), channels_last:
+ *   v = x[p][c], or swish(v) = v * sigmoid(v) if act == 3 (act 0: none)
+ *   out[p][c] = v                       (if out: the fp32 activation)
+ *   v = fp32(gate[img][c] * v)          (if gate: the squeeze-excite sigmoid, [n][c] fp32)
+ *   codes[p][c] = TR(v; sf, bitwidth, num_keep_terms)   [n][h][w][cp] as tq_act_encode
+ * x, out: [n][h][w][c] fp32, 16-byte aligned; 0 < sf < inf.
  */
-int tq_act_encode_gated(const float *x, int64_t n, int64_t c, int64_t h, int64_t w,
-                        const float *gate, float sf, int32_t bitwidth, int32_t num_keep_terms,
-                        void *codes, int64_t cp, int32_t fmt, void *stream);
+int tq_act_encode_act(const float *x, int64_t n, int64_t c, int64_t h, int64_t w,
+                      const float *gate, int32_t act, float *out, float sf, int32_t bitwidth,
+                      int32_t num_keep_terms, void *codes, int64_t cp, int32_t fmt,
+                      void *stream);
 
 /* Rows the weight-code matrix of tq_conv2d_termpair must be padded to (a multiple of). */
 int64_t tq_conv2d_cout_align(void);
@@ -125,7 +129,6 @@ int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w
  *   y = y + residual[p][c]            (fp32, if residual; [P][cout] channels_last)
  *   y = max(y, 0)                     (if relu == 1; the stored out keeps a NaN, as torch.relu)
  *   y = min(max(y, 0), 6)             (if relu == 2: ReLU6, MobileNet-V2; NaN kept likewise)
- *   y = y * (1 / (1 + exp(-y)))       (if relu == 3: swish, EfficientNet-b0; fp32 as torch)
  *   out[p][c] = y                     (if out)
  *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   format fmt_a, [P][cp_a] (if codes_a)
  *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   format fmt_b, [P][cp_b] (if codes_b)

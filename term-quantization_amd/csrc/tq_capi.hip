@@ -123,29 +123,32 @@ int tq_act_encode(const float* x, int32_t in_nhwc, int64_t n, int64_t c, int64_t
                     "act_encode launch");
 }
 
-int tq_act_encode_gated(const float* x, int64_t n, int64_t c, int64_t h, int64_t w,
-                        const float* gate, float sf, int32_t bitwidth, int32_t num_keep_terms,
-                        void* codes, int64_t cp, int32_t fmt, void* stream) {
+int tq_act_encode_act(const float* x, int64_t n, int64_t c, int64_t h, int64_t w,
+                      const float* gate, int32_t act, float* out, float sf, int32_t bitwidth,
+                      int32_t num_keep_terms, void* codes, int64_t cp, int32_t fmt,
+                      void* stream) {
   if (n < 0 || c < 1 || h < 0 || w < 0)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_gated: bad shape");
-  if (x == nullptr || gate == nullptr || codes == nullptr)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_gated: null buffer");
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: bad shape");
+  if (x == nullptr || codes == nullptr)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: null buffer");
+  if (act != 0 && act != tq::kActSwish)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: act must be 0 (none) or 3 (swish)");
   if (cp < c || cp % 8 != 0)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_gated: cp must be >= c and a multiple of 8");
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: cp must be >= c and a multiple of 8");
   if (fmt != TQ_CODES_I16 && fmt != TQ_CODES_F16)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_gated: unknown code format %d", fmt);
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: unknown code format %d", fmt);
   if (bitwidth < 0 || bitwidth > max_code_bits(fmt))
-    return fail(TQ_ERR_UNSUPPORTED, "act_encode_gated: codes need bitwidth <= %d (got %d)",
+    return fail(TQ_ERR_UNSUPPORTED, "act_encode_act: codes need bitwidth <= %d (got %d)",
                 max_code_bits(fmt), bitwidth);
   if (!(sf > 0.0f && sf <= 3.402823466e38f))
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_gated: sf must be finite and > 0");
-  if ((uintptr_t)codes % 16 != 0 || (uintptr_t)x % 16 != 0 || (uintptr_t)gate % 16 != 0)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_gated: buffers must be 16-byte aligned");
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: sf must be finite and > 0");
+  if ((uintptr_t)codes % 16 != 0 || (uintptr_t)x % 16 != 0 || (uintptr_t)out % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: x, out, codes must be 16-byte aligned");
   const int kk = num_keep_terms < 0 ? 0 : num_keep_terms;
-  return hip_status(tq::launch_act_encode_gated(x, gate, n, c, h, w, sf, bitwidth, kk,
-                                                static_cast<int16_t*>(codes), cp, fmt,
-                                                (hipStream_t)stream),
-                    "act_encode_gated launch");
+  return hip_status(tq::launch_act_encode_act(x, gate, act, out, n, c, h, w, sf, bitwidth, kk,
+                                              static_cast<int16_t*>(codes), cp, fmt,
+                                              (hipStream_t)stream),
+                    "act_encode_act launch");
 }
 
 int64_t tq_conv2d_cout_align(void) { return 128; }
@@ -257,9 +260,8 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->ch_scale = epi->ch_scale;
   a->ch_shift = epi->ch_shift;
   a->residual = epi->residual;
-  if (epi->relu < 0 || epi->relu > tq::kActSwish)
-    return fail(TQ_ERR_INVALID_ARGUMENT,
-                "conv2d: relu must be 0 (none), 1 (ReLU), 2 (ReLU6) or 3 (swish)");
+  if (epi->relu < 0 || epi->relu > 2)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: relu must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
   a->relu = epi->relu;
   a->codes_a = epi->codes_a;
   a->cp_a = (int)epi->cp_a;
@@ -275,8 +277,8 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
   a->k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
   a->fmt_b = epi->fmt_b;
-  a->lut_a = lut_entries(a->codes_a != nullptr, tq::act_nonneg(a->relu), a->inv_a, a->maxv_a);
-  a->lut_b = lut_entries(a->codes_b != nullptr, tq::act_nonneg(a->relu), a->inv_b, a->maxv_b);
+  a->lut_a = lut_entries(a->codes_a != nullptr, a->relu != 0, a->inv_a, a->maxv_a);
+  a->lut_b = lut_entries(a->codes_b != nullptr, a->relu != 0, a->inv_b, a->maxv_b);
   if (epi->config < 0 || epi->config > num_configs || epi->split_k < -1 || epi->split_k > 64)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
   if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)

@@ -164,17 +164,27 @@ __device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
   return (uint32_t)r + (__builtin_amdgcn_fractf(r) >= 0.5f ? 1u : 0u);
 }
 
-// Fused-epilogue activation (ConvArgs / DwConvArgs relu): 0 none, 1 ReLU, 2 ReLU6 (MobileNet-V2),
+// Fused-epilogue activation (DwConvArgs relu, tq_act_encode_act): 0 none, 1 ReLU, 2 ReLU6,
 // 3 swish y * sigmoid(y) (EfficientNet's MemoryEfficientSwish, with torch's fp32 sigmoid
 // 1 / (1 + exp(-y))).  y becomes the value the next layer's codes encode, o the stored value:
 // ReLU / ReLU6 keep a NaN in the stored value as torch.relu does (its codes are 0 either way:
 // TR(NaN) = 0).
 constexpr int kActSwish = 3;
 
+// Four instructions (v_exp_f32 of -y * log2(e), v_rcp_f32) instead of a full-precision expf
+// and an IEEE division: within ~1e-6 (relative) of torch's fp32 swish; the codes are TR of
+// the value stored.  (Used by the depthwise and encode kernels only: a swish branch in the
+// shared term-pair epilogue put the unrolled epilogue arrays of the strip and register-
+// staged engines into scratch, so EfficientNet's 1x1 convs store BN output and
+// tq_act_encode_act applies the swish.)
+__device__ __forceinline__ float swish_f32(float y) {
+  return y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y * -1.44269504f));
+}
+
 __device__ __forceinline__ void act_apply(int act, float& y, float& o) {
   o = y;
   if (act == kActSwish) {
-    y = y * (1.0f / (1.0f + expf(-y)));
+    y = swish_f32(y);
     o = y;
   } else if (act) {
     y = y > 0.0f ? y : 0.0f;

@@ -4,8 +4,7 @@
 //
 //   y = fp32(double(acc) * ch_scale[c] + ch_shift[c])   (conv scale, bias, folded eval BN)
 //     | fp32(double(acc) * scale + bias[c])
-//   y += residual (fp32), activation (ReLU / ReLU6 / swish: act_apply), fp32 store, next TR
-//   layers' activation codes
+//   y += residual (fp32), relu, fp32 store, next TR layers' activation codes
 //   (tr_layer.py:96-99 applied to y) in the consumer's code format.  ReLU propagates NaN
 //   into the stored value as torch.relu does; the codes of a NaN are 0, as TR(NaN) = 0.
 #pragma once
@@ -78,13 +77,20 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
   }
   float o[4];  // stored value: ReLU keeps NaN like torch.relu; the codes see 0 (TR(NaN) = 0)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) act_apply(a.relu, y[i], o[i]);
+  for (int i = 0; i < 4; ++i) {
+    o[i] = y[i];
+    if (a.relu) {
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;  // ReLU6 (MobileNet-V2)
+      o[i] = o[i] != o[i] ? o[i] : y[i];
+    }
+  }
   if (a.out)
     *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(o[0], o[1], o[2], o[3]);
   if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
-                               act_nonneg(a.relu), lut_a);
+                               a.relu, lut_a);
   if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
-                               act_nonneg(a.relu), lut_b);
+                               a.relu, lut_b);
 }
 
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
@@ -114,7 +120,14 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
   }
   float o[4];  // as emit4_nhwc_res: NaN-propagating ReLU for the stored value
 #pragma unroll
-  for (int i = 0; i < 4; ++i) act_apply(a.relu, y[i], o[i]);
+  for (int i = 0; i < 4; ++i) {
+    o[i] = y[i];
+    if (a.relu) {
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;  // ReLU6 (MobileNet-V2)
+      o[i] = o[i] != o[i] ? o[i] : y[i];
+    }
+  }
   if (a.out) {
     float* dst = a.out + p * a.Cout + co;
     if (vec) {
@@ -126,9 +139,9 @@ __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
     }
   }
   if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
-                               act_nonneg(a.relu), lut_a);
+                               a.relu, lut_a);
   if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
-                               act_nonneg(a.relu), lut_b);
+                               a.relu, lut_b);
 }
 
 // Epilogue code tables of a conv launch in LDS at `base` (a.lut_a then a.lut_b entries),

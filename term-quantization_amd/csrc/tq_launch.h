@@ -130,9 +130,10 @@ struct PoolArgs {
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream);
 
-hipError_t launch_act_encode_gated(const float* x, const float* gate, int64_t N, int64_t C,
-                                   int64_t H, int64_t W, float sf, int bitwidth, int k,
-                                   int16_t* codes, int64_t Cp, int fmt, hipStream_t stream);
+hipError_t launch_act_encode_act(const float* x, const float* gate, int act, float* out,
+                                 int64_t N, int64_t C, int64_t H, int64_t W, float sf,
+                                 int bitwidth, int k, int16_t* codes, int64_t Cp, int fmt,
+                                 hipStream_t stream);
 hipError_t launch_act_encode(const float* x, int in_nhwc, int64_t N, int64_t C, int64_t H,
                              int64_t W, float sf, int bitwidth, int k, int16_t* codes, int64_t Cp,
                              int fmt, hipStream_t stream);

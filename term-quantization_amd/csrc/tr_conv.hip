@@ -417,52 +417,68 @@ __global__ __launch_bounds__(256) void act_encode_kernel(const float* __restrict
       make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
 }
 
-// Squeeze-excite gate + TR (EfficientNet MBConvBlock.forward: x = sigmoid(x_sq) * x, then the
-// project conv's input TR): codes[p][c] = TR(fp32(gate[img][c] * x[p][c])), x fp32 NHWC with
-// C % 8 == 0 == Cp - C handled by the zero pad channels.  One lane per 8 channels of a pixel.
-__global__ __launch_bounds__(256) void act_encode_gated_kernel(
-    const float* __restrict__ x, const float* __restrict__ gate, int16_t* __restrict__ codes,
-    int64_t npix, int64_t HW, int C, int Cp, double inv_sf, float maxv, int k, int fmt) {
+// Activation / squeeze-excite gate + TR of EfficientNet-b0's MBConv tensors (channels_last,
+// one lane per 8 channels of a pixel): v = act(x) (none or swish, act_apply), out = v (if
+// out: the fp32 activation), v = fp32(gate[img][c] * v) (if gate: MBConvBlock.forward's
+// x = sigmoid(x_sq) * x), codes[p][c] = TR(v) for the next conv (pad channels zero).
+__global__ __launch_bounds__(256) void act_encode_act_kernel(
+    const float* __restrict__ x, const float* __restrict__ gate, int act, float* __restrict__ out,
+    int16_t* __restrict__ codes, int64_t npix, int64_t HW, int C, int Cp, double inv_sf,
+    float maxv, int k, int fmt) {
   const int chunks = Cp / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= npix * chunks) return;
   const int64_t pix = t / chunks;
   const int c0 = (int)(t - pix * chunks) * 8;
   const int64_t img = pix / HW;
-  uint32_t b[8];
-  if (c0 + 8 <= C && (C & 3) == 0) {
+  float v[8];
+  const bool vec = c0 + 8 <= C && (C & 3) == 0;
+  if (vec) {
     const float4 x0 = *reinterpret_cast<const float4*>(x + pix * C + c0);
     const float4 x1 = *reinterpret_cast<const float4*>(x + pix * C + c0 + 4);
-    const float4 g0 = *reinterpret_cast<const float4*>(gate + img * C + c0);
-    const float4 g1 = *reinterpret_cast<const float4*>(gate + img * C + c0 + 4);
-    const float xs[8] = {g0.x * x0.x, g0.y * x0.y, g0.z * x0.z, g0.w * x0.w,
-                         g1.x * x1.x, g1.y * x1.y, g1.z * x1.z, g1.w * x1.w};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = code_bits(tr_value_g1_inv(xs[i], inv_sf, maxv, k), fmt);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      b[i] = c < C ? code_bits(tr_value_g1_inv(gate[img * C + c] * x[pix * C + c], inv_sf, maxv,
-                                               k), fmt)
-                   : 0u;
+    for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? x[pix * C + c0 + i] : 0.0f;
+  }
+  float o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) act_apply(act, v[i], o[i]);
+  if (out) {
+    if (vec) {
+      *reinterpret_cast<float4*>(out + pix * C + c0) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(out + pix * C + c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (c0 + i < C) out[pix * C + c0 + i] = o[i];
     }
   }
+  if (gate) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? gate[img * C + c0 + i] * v[i] : 0.0f;
+  }
+  uint32_t b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    b[i] = c0 + i < C ? code_bits(tr_value_g1_inv(v[i], inv_sf, maxv, k), fmt) : 0u;
   *reinterpret_cast<uint4*>(codes + pix * Cp + c0) =
       make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
 }
 
 }  // namespace
 
-hipError_t launch_act_encode_gated(const float* x, const float* gate, int64_t N, int64_t C,
-                                   int64_t H, int64_t W, float sf, int bitwidth, int k,
-                                   int16_t* codes, int64_t Cp, int fmt, hipStream_t stream) {
+hipError_t launch_act_encode_act(const float* x, const float* gate, int act, float* out,
+                                 int64_t N, int64_t C, int64_t H, int64_t W, float sf,
+                                 int bitwidth, int k, int16_t* codes, int64_t Cp, int fmt,
+                                 hipStream_t stream) {
   const float maxv = (float)((1u << bitwidth) - 1u);
   const int64_t npix = N * H * W;
   const int64_t n = npix * (Cp / 8);
   if (n == 0) return hipSuccess;
-  act_encode_gated_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
-      x, gate, codes, npix, H * W, (int)C, (int)Cp, 1.0 / (double)sf, maxv, k, fmt);
+  act_encode_act_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
+      x, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, 1.0 / (double)sf, maxv, k, fmt);
   return hipGetLastError();
 }
 

@@ -101,7 +101,12 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
   for (int e = 0; e < 4; ++e) {
     y[e] = (float)((double)(int)acc4[e] * ep.sc + ep.sh);
     if (RES) y[e] += rv[e];  // (no + 0.0f without one: -0.0 stays, as in tq_epilogue.h)
-    act_apply(a.relu, y[e], o[e]);  // (the stored value keeps a NaN, as torch.relu)
+    o[e] = y[e];
+    if (a.relu) {
+      y[e] = y[e] > 0.0f ? y[e] : 0.0f;
+      if (a.relu == 2) y[e] = y[e] < 6.0f ? y[e] : 6.0f;  // ReLU6
+      o[e] = o[e] != o[e] ? o[e] : y[e];  // the stored value keeps a NaN (torch.relu)
+    }
   }
   if (OUT) {
 #pragma unroll
@@ -353,8 +358,8 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
   }
   ep.npeel_a = a.codes_a ? relu_peels(a.maxv_a, a.k_a) : 0;
   ep.npeel_b = a.codes_b ? relu_peels(a.maxv_b, a.k_b) : 0;
-  ep.fast_a = act_nonneg(a.relu) && a.inv_a > 0.0 && a.inv_a <= 1.0e308;
-  ep.fast_b = act_nonneg(a.relu) && a.inv_b > 0.0 && a.inv_b <= 1.0e308;
+  ep.fast_a = a.relu && a.inv_a > 0.0 && a.inv_a <= 1.0e308;
+  ep.fast_b = a.relu && a.inv_b > 0.0 && a.inv_b <= 1.0e308;
 
   // this lane's weight row (B fragments) and its swizzle key ((32 cb + r32) >> 1) & 7
   const u32x4* wrow_ptr = wl + co_l * kStripKU;

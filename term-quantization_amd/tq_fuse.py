@@ -525,9 +525,11 @@ class FusedMobileNetV2(nn.Module):
 #   [expand 1x1 -> BN -> swish] -> dw kxk (static same padding) -> BN -> swish
 #   -> squeeze-excite: x * sigmoid(se_expand(swish(se_reduce(avgpool(x)))))
 #   -> project 1x1 -> BN (+ identity)
-# The expand conv's epilogue applies BN + swish and writes the dw conv's codes; the dw
-# kernel applies BN + swish and writes the fp32 tensor the squeeze-excite branch pools; the
-# gate and the project conv's input TR are one pass (tq_act_encode_gated); the project
+# The expand conv's epilogue applies BN and stores fp32, one pass applies the swish and
+# writes the dw conv's codes (tq_act_encode_act; a swish branch inside the shared term-pair
+# epilogue cost the ResNet/MobileNet engines registers); the dw kernel applies
+# BN + swish and writes the fp32 tensor the squeeze-excite branch pools; the gate and the
+# project conv's input TR are one pass (tq_act_encode_act with the gate); the project
 # conv's epilogue adds BN and the identity and writes the next block's codes.  The squeeze-
 # excite convs themselves (1x1 on [N, C, 1, 1], 16-bit weights: the module's term-pair
 # "wide" kernel) and the pooling stay module calls: a few KB per image.
@@ -604,12 +606,18 @@ class FusedEfficientNet(nn.Module):
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             if b.expand is not None:
-                h, hcodes, _ = b.expand(codes, out=True if keep else None, relu="swish",
-                                        next_a=b.dw.consumer)
+                h, _, _ = b.expand(codes, out=True, relu=False)  # BN, fp32
+                dwc = b.dw.consumer
+                hcodes = torch.empty((h.shape[0], h.shape[2], h.shape[3], dwc.cp_in),
+                                     dtype=dwc.code_dtype, device=x.device)
+                hs = torch.empty_like(h) if keep else None
+                tq_ops._launch("act_encode_act", 6 * h.numel(),
+                               lambda: tq_native.act_encode_act(h, *dwc.quant, hcodes,
+                                                                act="swish", out=hs))
                 if keep:
                     capture.append({"name": "block%d.expand" % i, "kind": "conv",
                                     "conv": b.expand, "codes_in": codes, "residual": None,
-                                    "out": h, "codes_out": hcodes, "act": "swish"})
+                                    "out": h, "post": hs, "codes_out": hcodes, "act": None})
             else:
                 hcodes = codes
             if b.has_se:
@@ -617,9 +625,9 @@ class FusedEfficientNet(nn.Module):
                 g = b.gate(d)
                 pcodes = torch.empty((d.shape[0], d.shape[2], d.shape[3], b.project.cp_in),
                                      dtype=b.project.code_dtype, device=x.device)
-                tq_ops._launch("act_encode_gated", 4 * d.numel() + 2 * pcodes.numel(),
-                               lambda: tq_native.act_encode_gated(d, g, *b.project.quant,
-                                                                  pcodes))
+                tq_ops._launch("act_encode_act", 6 * d.numel(),
+                               lambda: tq_native.act_encode_act(d, *b.project.quant, pcodes,
+                                                                gate=g))
             else:
                 d, pcodes = b.dw(hcodes, b.project, out=keep, act="swish")
                 g = None
@@ -638,10 +646,10 @@ class FusedEfficientNet(nn.Module):
                                 "residual": xin if b.use_res else None, "out": xout,
                                 "codes_out": codes, "act": None})
             xin = xout
-        y, _, _ = self.head(codes, out=True, relu="swish")
+        y, _, _ = self.head(codes, out=True, relu=False)
         if keep:
             capture.append({"name": "head", "kind": "conv", "conv": self.head,
                             "codes_in": codes, "residual": None, "out": y, "codes_out": None,
-                            "act": "swish"})
-        y = m._avg_pooling(y).flatten(start_dim=1)
+                            "act": None})
+        y = m._avg_pooling(m._swish(y)).flatten(start_dim=1)
         return m._fc(m._dropout(y))

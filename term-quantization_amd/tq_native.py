@@ -39,8 +39,8 @@ _SIGNATURES = {
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
                          _vp],
-    "tq_act_encode_gated": [_vp, _i64, _i64, _i64, _i64, _vp, _f32, _i32, _i32, _vp, _i64,
-                            _i32, _vp],
+    "tq_act_encode_act": [_vp, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _f32, _i32, _i32, _vp,
+                          _i64, _i32, _vp],
     "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _i32,
                       _vp],
     "tq_conv2d_cout_align": [],
@@ -135,6 +135,8 @@ def lib():
                         "`make -C term-quantization_amd` (there is no CPU fallback)" % LIB_PATH)
                 l = ctypes.CDLL(LIB_PATH)
                 for name, argtypes in _SIGNATURES.items():
+                    if os.environ.get("TQ_LIB_PATH") and not hasattr(l, name):
+                        continue  # an older A/B build (tools only) may lack newer entries
                     fn = getattr(l, name)
                     fn.argtypes = argtypes
                     fn.restype = _RESTYPE.get(name, ctypes.c_int)
@@ -265,22 +267,28 @@ def act_code(relu):
     "swish" swish (EfficientNet)."""
     if relu == "swish":
         return 3
+    if relu is None:
+        return 0
     return 2 if relu == 6 else int(bool(relu))
 
 
-def act_encode_gated(x, gate, sf, bitwidth, num_keep_terms, codes):
-    """codes = TR(gate[n, c] * x) (tq_act_encode_gated): x fp32 channels_last [N, C, H, W],
-    gate fp32 [N, C] -- EfficientNet's squeeze-excite scaling fused into the project conv's
-    input TR."""
+def act_encode_act(x, sf, bitwidth, num_keep_terms, codes, act=None, gate=None, out=None):
+    """codes = TR(gate[n, c] * act(x)) (tq_act_encode_act): x fp32 channels_last [N, C, H, W],
+    act None or "swish", gate None or fp32 [N, C] (EfficientNet's squeeze-excite sigmoid),
+    ``out`` (optional, channels_last like x) receives act(x)."""
     n, c, h, w = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
-        raise RuntimeError("act_encode_gated: x must be channels_last")
-    if gate.dtype != torch.float32 or tuple(gate.shape) != (n, c) or not gate.is_contiguous():
-        raise RuntimeError("act_encode_gated: gate must be a contiguous fp32 [N, C] tensor")
+        raise RuntimeError("act_encode_act: x must be channels_last")
+    if gate is not None and (gate.dtype != torch.float32 or tuple(gate.shape) != (n, c) or
+                             not gate.is_contiguous()):
+        raise RuntimeError("act_encode_act: gate must be a contiguous fp32 [N, C] tensor")
+    if out is not None and (out.shape != x.shape or
+                            not out.is_contiguous(memory_format=torch.channels_last)):
+        raise RuntimeError("act_encode_act: out must be channels_last like x")
     with torch.cuda.device(x.device):
-        rc = lib().tq_act_encode_gated(_ptr(x), n, c, h, w, _ptr(gate), sf, bitwidth,
-                                       num_keep_terms, _ptr(codes), codes.shape[-1],
-                                       code_format(codes), _stream(x))
+        rc = lib().tq_act_encode_act(_ptr(x), n, c, h, w, _ptr(gate), act_code(act), _ptr(out),
+                                     sf, bitwidth, num_keep_terms, _ptr(codes), codes.shape[-1],
+                                     code_format(codes), _stream(x))
     _check(rc)
     return codes
 

@@ -7,8 +7,10 @@ sample of images,
        composition conv (static same padding) -> BN -> (swish | + identity) of the very
        codes it consumed (tr_layer.py:124-126 + efficientnet_pytorch's MBConvBlock), and
   (ii) the codes it emitted are bit-exact oracle.tr() of its stored fp32 output -- for the
-       depthwise layers, of fp32(gate * output) with the squeeze-excite gate (the project
-       conv's input, MBConvBlock.forward: x = sigmoid(x_sq) * x).
+       expand convs, of the swish the encode pass stored (itself within 1e-6 of the fp64
+       swish of the conv output), for the depthwise layers of fp32(gate * output) with the
+       squeeze-excite gate (the project conv's input, MBConvBlock.forward:
+       x = sigmoid(x_sq) * x).
 The bench-mode logits are bit-identical to the capture-mode ones."""
 import numpy as np
 import pytest
@@ -109,6 +111,12 @@ def test_fused_efficientnet_b0_teacher_forced(net):
         y = _nchw(rec["out"], SAMPLE)
         err = (y - ref).abs()
         assert bool((err <= bound + 1e-30).all()), (rec["name"], float((err / bound).max()))
+        if rec.get("post") is not None:  # the swish pass after an expand conv's BN output
+            post = _nchw(rec["post"], SAMPLE)
+            sw = y * torch.sigmoid(y)
+            assert bool(((post - sw).abs() <= 1e-6 * sw.abs() + 1e-7 * y.abs() + 1e-30).all()), \
+                rec["name"]
+            y = post
         if rec["codes_out"] is None:
             continue
         quant = _consumer_quant(cap, rec["codes_out"])

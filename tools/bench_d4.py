@@ -62,7 +62,7 @@ def kernel_breakdown(fn, steps, total_s):
             tf = 2 * k["work"] / k["seconds"] / 1e12
             e.update({"bound": "mfma", "achieved_tflops": tf, "peak_tflops": MFMA_F16_PEAK_TFLOPS,
                       "frac": tf / MFMA_F16_PEAK_TFLOPS})
-        elif name in ("act_encode", "act_encode_gated"):
+        elif name in ("act_encode", "act_encode_act"):
             gbs = k["work"] / k["seconds"] / 1e9
             e.update({"bound": "hbm", "achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
                       "frac": gbs / HBM_PEAK_GBS})
