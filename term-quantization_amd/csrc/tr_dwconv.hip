@@ -10,6 +10,8 @@
 // activation tile is re-read from cache per tap, the output written once.
 // Padding is implicit (any tap outside the input reads 0), so asymmetric "same" padding
 // (Conv2dStaticSamePadding) is expressed by pad_top / pad_left and the output size.
+#include <stdlib.h>
+
 #include "tq_device.h"
 #include "tq_launch.h"
 
@@ -20,48 +22,11 @@ namespace {
 // Operands known to fit 24 signed bits let the compiler emit v_mad_i32_i24 (full rate).
 __device__ __forceinline__ int sext24(int v) { return (v << 8) >> 8; }
 
-__global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
-  if (a.lut_c) {
-    lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
-    __syncthreads();
-  }
-  const int chunks = a.Cp / 8;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
-  if (t >= P * chunks) return;
-  const int64_t p = t / chunks;
-  const int c0 = (int)(t - p * chunks) * 8;
+// Epilogue of output pixel p (image img, in-image index rem), channels c0 .. c0 + 7, from the
+// exact int32 sums: one fp64 -> fp32 rounding, activation, fp32 store and/or next codes.
+__device__ __forceinline__ void dw_emit8(const DwConvArgs& a, const uint16_t* lut, int64_t p,
+                                         int64_t img, int rem, int c0, const int acc[8]) {
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
-  const int64_t img = p / HoWo;
-  const int rem = (int)(p - img * HoWo);
-  const int oh = rem / a.Wo;
-  const int ow = rem - oh * a.Wo;
-  int acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0;
-  for (int r = 0; r < a.KH; ++r) {
-    const int ih = oh * a.sh - a.ph + r * a.dh;
-    if (ih < 0 || ih >= a.H) continue;
-    for (int s = 0; s < a.KW; ++s) {
-      const int iw = ow * a.sw - a.pw + s * a.dw;
-      if (iw < 0 || iw >= a.W) continue;
-      const int4 xv =
-          *reinterpret_cast<const int4*>(a.x + ((img * a.H + ih) * a.W + iw) * a.Cp + c0);
-      const int32_t* wt = a.w + (int64_t)(r * a.KW + s) * a.Cp + c0;
-      const int4 w0 = *reinterpret_cast<const int4*>(wt);
-      const int4 w1 = *reinterpret_cast<const int4*>(wt + 4);
-      const int xs[4] = {xv.x, xv.y, xv.z, xv.w};
-      const int ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int lo = (int)(short)(xs[i] & 0xFFFF);
-        const int hi = xs[i] >> 16;
-        acc[2 * i] += lo * sext24(ws[2 * i]);
-        acc[2 * i + 1] += hi * sext24(ws[2 * i + 1]);
-      }
-    }
-  }
   float y[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -123,11 +88,137 @@ __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
+  if (a.lut_c) {
+    lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
+    __syncthreads();
+  }
+  const int chunks = a.Cp / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+  if (t >= P * chunks) return;
+  const int64_t p = t / chunks;
+  const int c0 = (int)(t - p * chunks) * 8;
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  const int64_t img = p / HoWo;
+  const int rem = (int)(p - img * HoWo);
+  const int oh = rem / a.Wo;
+  const int ow = rem - oh * a.Wo;
+  int acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0;
+  for (int r = 0; r < a.KH; ++r) {
+    const int ih = oh * a.sh - a.ph + r * a.dh;
+    if (ih < 0 || ih >= a.H) continue;
+    for (int s = 0; s < a.KW; ++s) {
+      const int iw = ow * a.sw - a.pw + s * a.dw;
+      if (iw < 0 || iw >= a.W) continue;
+      const int4 xv =
+          *reinterpret_cast<const int4*>(a.x + ((img * a.H + ih) * a.W + iw) * a.Cp + c0);
+      const int32_t* wt = a.w + (int64_t)(r * a.KW + s) * a.Cp + c0;
+      const int4 w0 = *reinterpret_cast<const int4*>(wt);
+      const int4 w1 = *reinterpret_cast<const int4*>(wt + 4);
+      const int xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      const int ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int lo = (int)(short)(xs[i] & 0xFFFF);
+        const int hi = xs[i] >> 16;
+        acc[2 * i] += lo * sext24(ws[2 * i]);
+        acc[2 * i + 1] += hi * sext24(ws[2 * i + 1]);
+      }
+    }
+  }
+  dw_emit8(a, a.lut_c ? lut : nullptr, p, img, rem, c0, acc);
+}
+
+// Row-blocked variant for KH x KW taps known at compile time (3x3, 5x5, dilation 1): a lane
+// owns channels c0 .. c0 + 7 of kDwRows vertically adjacent output pixels, so each tap's
+// weights are loaded once for kDwRows outputs and every load of a tap row is issued
+// unrolled (no per-tap dependent branch chain).  Lanes run chunk-fastest, then along the
+// output row: a wave's loads of one tap cover contiguous NHWC bytes.
+constexpr int kDwRows = 4;
+
+template <int KH, int KW>
+__global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
+  if (a.lut_c) {
+    lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
+    __syncthreads();
+  }
+  const int chunks = a.Cp / 8;
+  const int hb = (a.Ho + kDwRows - 1) / kDwRows;  // row blocks per image
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t lanes = (int64_t)a.N * hb * a.Wo * chunks;
+  if (t >= lanes) return;
+  int64_t q = t / chunks;
+  const int c0 = (int)(t - q * chunks) * 8;
+  const int ow = (int)(q % a.Wo);
+  q /= a.Wo;
+  const int bh = (int)(q % hb);
+  const int64_t img = q / hb;
+  const int oh0 = bh * kDwRows;
+  const int iw0 = ow * a.sw - a.pw;
+  int acc[kDwRows][8];
+#pragma unroll
+  for (int r = 0; r < kDwRows; ++r)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[r][i] = 0;
+  const int16_t* xb = a.x + img * a.H * a.W * a.Cp + c0;
+#pragma unroll
+  for (int kr = 0; kr < KH; ++kr) {
+#pragma unroll
+    for (int ks = 0; ks < KW; ++ks) {
+      const int iw = iw0 + ks;
+      if (iw < 0 || iw >= a.W) continue;
+      const int32_t* wt = a.w + (int64_t)(kr * KW + ks) * a.Cp + c0;
+      const int4 w0 = *reinterpret_cast<const int4*>(wt);
+      const int4 w1 = *reinterpret_cast<const int4*>(wt + 4);
+      const int ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int r = 0; r < kDwRows; ++r) {
+        const int ih = (oh0 + r) * a.sh - a.ph + kr;
+        if (ih < 0 || ih >= a.H) continue;
+        const int4 xv = *reinterpret_cast<const int4*>(xb + ((int64_t)ih * a.W + iw) * a.Cp);
+        const int xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lo = (int)(short)(xs[i] & 0xFFFF);
+          const int hi = xs[i] >> 16;
+          acc[r][2 * i] += lo * sext24(ws[2 * i]);
+          acc[r][2 * i + 1] += hi * sext24(ws[2 * i + 1]);
+        }
+      }
+    }
+  }
+  const uint16_t* l = a.lut_c ? lut : nullptr;
+#pragma unroll
+  for (int r = 0; r < kDwRows; ++r) {
+    const int oh = oh0 + r;
+    if (oh >= a.Ho) break;
+    const int rem = oh * a.Wo + ow;
+    dw_emit8(a, l, (img * a.Ho + oh) * a.Wo + ow, img, rem, c0, acc[r]);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.N * a.Ho * a.Wo * (a.Cp / 8);
   if (n == 0) return hipSuccess;
+  static const char* rows = getenv("TQ_DW_ROWS");  // A/B override (tools only): 0 off
+  if (!(rows && atoi(rows) == 0) && a.dh == 1 && a.dw == 1 &&
+      ((a.KH == 3 && a.KW == 3) || (a.KH == 5 && a.KW == 5))) {
+    const int64_t lanes =
+        (int64_t)a.N * ((a.Ho + kDwRows - 1) / kDwRows) * a.Wo * (a.Cp / 8);
+    const dim3 grid((unsigned)((lanes + 255) / 256));
+    if (a.KH == 3)
+      dwconv_tp_rows_kernel<3, 3><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
+    else
+      dwconv_tp_rows_kernel<5, 5><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
+    return hipGetLastError();
+  }
   dwconv_tp_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, (size_t)a.lut_c * 2, stream>>>(a);
   return hipGetLastError();
 }
