@@ -87,6 +87,28 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
+def timed_graph(fn, steps, warmup):
+    """fn captured once as a hipGraph and replayed (no per-kernel host launches); None when
+    the capture fails."""
+    try:
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        g.replay()
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 -- reported as None
+        torch.cuda.synchronize()
+        return None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
 def lstm(args, dev):
     torch.manual_seed(1111)
     ntokens, bsz, bptt = evaluate_lstm.WT2_VOCAB, 10, 35
@@ -156,8 +178,12 @@ def cnn(arch, args, dev):
             ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
                   tq_fuse.FusedEfficientNet)(q)
             tf = timed(lambda: ex(x), args.steps, args.warmup)
+            tg = timed_graph(lambda: ex(x), args.steps, args.warmup)
             fused = {"images_per_s": args.batch / tf, "ms_per_step": tf * 1e3,
                      "term_pair_macs_per_s": tmacs * args.batch / tf,
+                     # the same forward replayed as one hipGraph: with ~50 launches of
+                     # ~100 us the eager loop is partly host-bound
+                     "images_per_s_graph": args.batch / tg if tg else None,
                      "kernels": kernel_breakdown(lambda: ex(x), args.steps, tf)}
     modes = sorted({m.mode for m in q.modules() if isinstance(m, tr_layer.TRConv2dLayer)})
     return {"metric": "%s TQ images/s" % arch, "value": args.batch / t, "unit": "images/s",
