@@ -15,7 +15,8 @@
 //
 //   workgroup = 4 waves, tile 64*MB (Cout) x 128 (output pixels), MB = 1 or 2
 //   wave      = 64*MB x 32: 2*MB MFMA blocks of 32 x 32, 8*MB MFMAs per K-step
-//   K-step    = 64 codes of one filter tap (Cp % 64 == 0)
+//   K-step    = 64 codes of one filter tap (Cp % 64 == 0; 1x1 convs: any Cp, the last step
+//               zero-padded)
 //   A (weights [Cout_pad][Kp] fp16): global_load_lds_dwordx4 into a 3-slot ring, 8 KB/slot,
 //             rows swizzled chunk ^= (row >> 1) & 7 on the source side (conflict-free reads)
 //   B (activation codes [N][H][W][Cp] fp16): lane (r32, hh) loads, per block column and
@@ -150,8 +151,13 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
              lds + slot * C::SLOT + (wave * C::AI + i) * 64);
     const bool ok = (tmask >> i_tap) & 1ull;
     const uint16_t* src = ok ? xsrc + (boff + i_toff) : zero;
+    // codes of the lane's pixel left in this tap from its first (8-code) group: >= 56 except
+    // in the partial last K-step of a 1x1 conv with Cp % 64 != 0, whose groups past Cp
+    // (another pixel's channels) read the zero page instead
+    const int cleft = cur_cp - i_cb - 8 * hh;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) b[s] = *reinterpret_cast<const u32x4*>(src + 16 * s);
+    for (int s = 0; s < 4; ++s)
+      b[s] = *reinterpret_cast<const u32x4*>((16 * s < cleft ? src : zero) + 16 * s);
     ++i_st;
     i_cb += kKStep;
     i_toff += kKStep;
@@ -361,8 +367,11 @@ hipError_t launch_direct_mb(const ConvArgs& a, hipStream_t stream) {
 
 }  // namespace
 
+// Cp % 64 == 0, or a 1x1 conv with any Cp (% 8 == 0): its K-steps walk the zero-padded
+// weight rows (Kp = roundup(Cp, 64)) and the last one reads the zero page past Cp.
 bool conv_direct_eligible(const ConvArgs& a, int out_nhwc) {
-  return out_nhwc && a.Cp % kKStep == 0 && a.KH * a.KW <= 64 && a.Kp % kKStep == 0 &&
+  return out_nhwc && (a.Cp % kKStep == 0 || (a.KH * a.KW == 1 && a.Cp % 8 == 0)) &&
+         a.KH * a.KW <= 64 && a.Kp % kKStep == 0 &&
          (a.ds_x == nullptr || a.ds_Cp % kKStep == 0);
 }
 

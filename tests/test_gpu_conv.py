@@ -179,6 +179,25 @@ def test_mfma_patch_engine_bit_identical_to_valu(shape):
     assert torch.equal(ym, yv)
 
 
+@pytest.mark.parametrize("shape", [
+    # n, cin, h, w, cout, stride -- 1x1 convs with Cp % 64 != 0: the direct engine's
+    # zero-padded last K-step (MobileNet-V2 / EfficientNet-b0 expand and project shapes)
+    (3, 24, 14, 14, 144, 1),
+    (2, 96, 9, 9, 24, 1),
+    (2, 144, 8, 8, 40, 2),
+    (1, 160, 7, 7, 960, 1),
+    (4, 40, 5, 5, 240, 1),
+    (2, 8, 6, 6, 16, 1),
+])
+def test_mfma_direct_1x1_partial_chunk_bit_identical_to_valu(shape):
+    n, cin, h, w_, cout, s = shape
+    torch.manual_seed(sum(shape))
+    x = torch.relu(torch.randn(n, cin, h, w_, device=DEV)).to(memory_format=torch.channels_last)
+    lay, ym, yv = _engines_pair(cin, cout, 1, s, 0, x, 9, 3, 9, 8, 12, 0.02, seed=sum(shape))
+    assert lay.w_codes.shape[1] % 64 == 0
+    assert torch.equal(ym, yv)
+
+
 def test_mfma_flush_window_exact_at_extremes():
     """Saturated activations (every code 511) against constant maximal weights (every code
     256): one K-step of products is 2^23, so the fp32 accumulators must be flushed every 2
