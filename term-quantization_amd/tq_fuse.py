@@ -309,8 +309,8 @@ class FusedResNet(nn.Module):
         return torch.cat([r[0] for r in res])
 
     def _steps(self, x, capture, result):
-        """forward() as a generator: yields after each kernel launch; the logits end up in
-        result[0]."""
+        """forward() as a generator: yields after each kernel launch (the block index after a
+        block's last conv, else None); the logits end up in result[0]."""
         m = self.qmodel
         keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
@@ -347,7 +347,7 @@ class FusedResNet(nn.Module):
                 relu=True, next_a=nxt.conv1 if nxt else None,
                 next_b=None if shared else next_b,
                 downsample=(b.down, codes_down) if fuse_ds else None)
-            yield
+            yield i  # block i done
             if shared:
                 codes_down = codes
             if keep:
