@@ -19,6 +19,8 @@ namespace tq {
 
 namespace {
 
+__device__ int4 g_dw_zero;  // zero-initialised static storage, never written: padding taps
+
 // Operands known to fit 24 signed bits let the compiler emit v_mad_i32_i24 (full rate).
 __device__ __forceinline__ int sext24(int v) { return (v << 8) >> 8; }
 
@@ -166,12 +168,15 @@ __global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[r][i] = 0;
   const int16_t* xb = a.x + img * a.H * a.W * a.Cp + c0;
-#pragma unroll
+  // every load is unconditional (taps in the padding read a zero block): all of a tap row's
+  // loads issue back to back instead of one branch-guarded round trip per tap (one tap row
+  // at a time: unrolling the rows too holds every load in flight, 244+ VGPRs)
+#pragma unroll 1
   for (int kr = 0; kr < KH; ++kr) {
 #pragma unroll
     for (int ks = 0; ks < KW; ++ks) {
       const int iw = iw0 + ks;
-      if (iw < 0 || iw >= a.W) continue;
+      const bool wok = iw >= 0 && iw < a.W;
       const int32_t* wt = a.w + (int64_t)(kr * KW + ks) * a.Cp + c0;
       const int4 w0 = *reinterpret_cast<const int4*>(wt);
       const int4 w1 = *reinterpret_cast<const int4*>(wt + 4);
@@ -179,8 +184,11 @@ __global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
 #pragma unroll
       for (int r = 0; r < kDwRows; ++r) {
         const int ih = (oh0 + r) * a.sh - a.ph + kr;
-        if (ih < 0 || ih >= a.H) continue;
-        const int4 xv = *reinterpret_cast<const int4*>(xb + ((int64_t)ih * a.W + iw) * a.Cp);
+        const bool ok = wok && ih >= 0 && ih < a.H;
+        const int4* src = ok ? reinterpret_cast<const int4*>(
+                                   xb + ((int64_t)ih * a.W + iw) * a.Cp)
+                             : &g_dw_zero;
+        const int4 xv = *src;
         const int xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
