@@ -52,7 +52,6 @@ constexpr int kStripTaps = 9;       // 3 x 3
 constexpr int kStripKU = kStripTaps * kStripC / 8;  // 72 units of 8 codes per weight row
 constexpr int kStripWUnits = kStripC * kStripKU;    // 4608 units = 72 KB
 constexpr int kStripMaxW = 56;
-constexpr int kStripMaxBlk = 4;     // 32-pixel blocks per wave (tile <= 8 blocks)
 
 __host__ __device__ constexpr int strip_patch_px(int w) { return (kStripTR + 2) * w + 1; }
 
