@@ -129,6 +129,8 @@ int tq_conv2d_termpair(const int16_t *act_codes, int64_t n, int64_t h, int64_t w
  *   y = y + residual[p][c]            (fp32, if residual; [P][cout] channels_last)
  *   y = max(y, 0)                     (if relu == 1; the stored out keeps a NaN, as torch.relu)
  *   y = min(max(y, 0), 6)             (if relu == 2: ReLU6, MobileNet-V2; NaN kept likewise)
+ *   y = y * sigmoid(y)                (if relu == 3: swish, EfficientNet-b0; fp16 entry only,
+ *                                      1x1 convs or cp % 64 == 0: the direct engine)
  *   out[p][c] = y                     (if out)
  *   codes_a[p][c] = TR(y; sf_a, bits_a, terms_a)   format fmt_a, [P][cp_a] (if codes_a)
  *   codes_b[p][c] = TR(y; sf_b, bits_b, terms_b)   format fmt_b, [P][cp_b] (if codes_b)

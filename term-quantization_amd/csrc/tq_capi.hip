@@ -260,8 +260,9 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->ch_scale = epi->ch_scale;
   a->ch_shift = epi->ch_shift;
   a->residual = epi->residual;
-  if (epi->relu < 0 || epi->relu > 2)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: relu must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
+  if (epi->relu < 0 || epi->relu > tq::kActSwish)
+    return fail(TQ_ERR_INVALID_ARGUMENT,
+                "conv2d: relu must be 0 (none), 1 (ReLU), 2 (ReLU6) or 3 (swish)");
   a->relu = epi->relu;
   a->codes_a = epi->codes_a;
   a->cp_a = (int)epi->cp_a;
@@ -277,8 +278,8 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
   a->k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
   a->fmt_b = epi->fmt_b;
-  a->lut_a = lut_entries(a->codes_a != nullptr, a->relu != 0, a->inv_a, a->maxv_a);
-  a->lut_b = lut_entries(a->codes_b != nullptr, a->relu != 0, a->inv_b, a->maxv_b);
+  a->lut_a = lut_entries(a->codes_a != nullptr, tq::act_nonneg(a->relu), a->inv_a, a->maxv_a);
+  a->lut_b = lut_entries(a->codes_b != nullptr, tq::act_nonneg(a->relu), a->inv_b, a->maxv_b);
   if (epi->config < 0 || epi->config > num_configs || epi->split_k < -1 || epi->split_k > 64)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
   if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)
@@ -348,6 +349,8 @@ int tq_conv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, int
     return fail(TQ_ERR_UNSUPPORTED, "conv2d: a fused downsample needs the fp16 (MFMA) entry");
   rc = apply_epilogue(epi, cout, out, tq::conv_num_configs(), &a);
   if (rc != TQ_OK) return rc;
+  if (a.relu == tq::kActSwish)
+    return fail(TQ_ERR_UNSUPPORTED, "conv2d: the swish epilogue needs the fp16 (MFMA) entry");
   return hip_status(tq::launch_conv2d_tp(a, 1, (hipStream_t)stream), "conv2d launch");
 }
 
@@ -382,6 +385,9 @@ int tq_conv2d_termpair_f16(const uint16_t* act_codes, int64_t n, int64_t h, int6
     if (rc != TQ_OK) return rc;
     if (a.ds_x && (a.Cp % 64 != 0 || kh * kw > 64))
       return fail(TQ_ERR_UNSUPPORTED, "conv2d_f16: a fused downsample needs cp %% 64 == 0");
+    if (a.relu == tq::kActSwish && !(a.Cp % 64 == 0 || kh * kw == 1))
+      return fail(TQ_ERR_UNSUPPORTED,
+                  "conv2d_f16: the swish epilogue runs on the direct engine (1x1 or cp %% 64 == 0)");
   }
   return hip_status(tq::launch_conv2d_mfma(a, out_nhwc, (hipStream_t)stream),
                     "conv2d_f16 launch");

@@ -61,6 +61,10 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, i
 // downsample's identity, or zeros when there is neither): the epilogue issues every residual
 // load of a tile before its first store, so the loads' latency is paid once, not once per
 // output quad.  Cout % 4 == 0.
+// SWISH: the activation is swish (relu == 3; only the direct engine's SWISH instantiation,
+// so the other instantiations' code is unchanged -- a runtime swish branch here put the
+// strip and register-staged engines' epilogue arrays in scratch).
+template <bool SWISH = false>
 __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int co,
                                                const int acc[4], const double sc[4],
                                                const double sh[4], const float4 rv,
@@ -79,7 +83,10 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     o[i] = y[i];
-    if (a.relu) {
+    if (SWISH) {
+      y[i] = swish_f32(y[i]);
+      o[i] = y[i];
+    } else if (a.relu) {
       y[i] = y[i] > 0.0f ? y[i] : 0.0f;
       if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;  // ReLU6 (MobileNet-V2)
       o[i] = o[i] != o[i] ? o[i] : y[i];
@@ -88,9 +95,9 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
   if (a.out)
     *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(o[0], o[1], o[2], o[3]);
   if (a.codes_a) store_codes4(a.codes_a, a.cp_a, a.Cout, p, co, y, a.inv_a, a.maxv_a, a.k_a, a.fmt_a,
-                               a.relu, lut_a);
+                               SWISH ? false : (bool)a.relu, lut_a);
   if (a.codes_b) store_codes4(a.codes_b, a.cp_b, a.Cout, p, co, y, a.inv_b, a.maxv_b, a.k_b, a.fmt_b,
-                               a.relu, lut_b);
+                               SWISH ? false : (bool)a.relu, lut_b);
 }
 
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:

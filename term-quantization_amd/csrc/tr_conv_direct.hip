@@ -56,7 +56,7 @@ struct DirCfg {
 // main conv's, into fresh fp32 accumulators, while the main conv's sums wait in int32; the
 // epilogue turns them into the identity (what the separate downsample conv would store) and
 // adds it where a residual read from HBM would go.
-template <int MB, bool FLUSH, bool DS>
+template <int MB, bool FLUSH, bool DS, bool SWISH>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
   constexpr int NBM = 2 * MB;  // 32-row MFMA blocks per wave
@@ -343,17 +343,17 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     const u32x4 v = t[px * C::SL + (slot ^ (px & 15))];
     const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
     if (vec)
-      emit4_nhwc_res(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
+      emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
       emit4_nhwc(a, p, co, acc4, sc, sh, false, lut_a, lut_b);
   }
 }
 
-template <int MB, bool FLUSH, bool DS>
+template <int MB, bool FLUSH, bool DS, bool SWISH = false>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   using C = DirCfg<MB>;
   const int64_t tiles = ((a.P + C::BN - 1) / C::BN) * ((a.Cout + C::BM - 1) / C::BM);
-  conv2d_tp_direct_kernel<MB, FLUSH, DS>
+  conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH>
       <<<dim3((unsigned)tiles), kDirThreads, (size_t)conv_lut_bytes(a), stream>>>(a);
   return hipGetLastError();
 }
@@ -377,6 +377,12 @@ bool conv_direct_eligible(const ConvArgs& a, int out_nhwc) {
 
 // mb: 1 = 64 x 128 tiles, 2 = 128 x 128 tiles.
 hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream) {
+  if (a.relu == kActSwish) {  // swish epilogue (EfficientNet): 64-row tiles, no fused downsample
+    if (a.ds_x || (a.Cout & 3)) return hipErrorInvalidValue;
+    const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
+    return flush ? launch_direct_cfg<1, true, false, true>(a, stream)
+                 : launch_direct_cfg<1, false, false, true>(a, stream);
+  }
   if (a.ds_x)  // fused downsample: 64-row tiles (the second int32 tile costs registers)
     return launch_direct_mb<1, true>(a, stream);
   if (mb == 2) return launch_direct_mb<2, false>(a, stream);

@@ -494,6 +494,10 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   a.ab = ab ? atoi(ab) : 0;
   static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 MB
   if (cfg < 0 && dir && atoi(dir) > 0) cfg = atoi(dir) == 1 ? 9 : 8;
+  if (a.relu == kActSwish) {  // the swish epilogue exists on the direct engine only
+    if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
+    return launch_conv2d_direct(a, 1, stream);
+  }
   if (a.ds_x) {  // a fused downsample phase: the direct engine only
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
     return launch_conv2d_direct(a, 1, stream);

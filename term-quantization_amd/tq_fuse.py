@@ -525,9 +525,9 @@ class FusedMobileNetV2(nn.Module):
 #   [expand 1x1 -> BN -> swish] -> dw kxk (static same padding) -> BN -> swish
 #   -> squeeze-excite: x * sigmoid(se_expand(swish(se_reduce(avgpool(x)))))
 #   -> project 1x1 -> BN (+ identity)
-# The expand conv's epilogue applies BN and stores fp32, one pass applies the swish and
-# writes the dw conv's codes (tq_act_encode_act; a swish branch inside the shared term-pair
-# epilogue cost the ResNet/MobileNet engines registers); the dw kernel applies
+# The expand conv's epilogue applies BN + swish and writes the dw conv's codes (the direct
+# engine's swish instantiation: a runtime swish branch in the shared term-pair epilogue cost
+# the ResNet/MobileNet engines scratch); the dw kernel applies
 # BN + swish and writes the fp32 tensor the squeeze-excite branch pools; the gate and the
 # project conv's input TR are one pass (tq_act_encode_act with the gate); the project
 # conv's epilogue adds BN and the identity and writes the next block's codes.  The squeeze-
@@ -606,18 +606,14 @@ class FusedEfficientNet(nn.Module):
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             if b.expand is not None:
-                h, _, _ = b.expand(codes, out=True, relu=False)  # BN, fp32
-                dwc = b.dw.consumer
-                hcodes = torch.empty((h.shape[0], h.shape[2], h.shape[3], dwc.cp_in),
-                                     dtype=dwc.code_dtype, device=x.device)
-                hs = torch.empty_like(h) if keep else None
-                tq_ops._launch("act_encode_act", 6 * h.numel(),
-                               lambda: tq_native.act_encode_act(h, *dwc.quant, hcodes,
-                                                                act="swish", out=hs))
+                # BN + swish + the dw conv's codes in the epilogue (the direct engine's swish
+                # instantiation: 1x1 convs)
+                h, hcodes, _ = b.expand(codes, out=True if keep else None, relu="swish",
+                                        next_a=b.dw.consumer)
                 if keep:
                     capture.append({"name": "block%d.expand" % i, "kind": "conv",
                                     "conv": b.expand, "codes_in": codes, "residual": None,
-                                    "out": h, "post": hs, "codes_out": hcodes, "act": None})
+                                    "out": h, "codes_out": hcodes, "act": "swish"})
             else:
                 hcodes = codes
             if b.has_se:
