@@ -159,3 +159,30 @@ def test_lstm_cell_argument_validation():
     assert b"null" in lib.tq_last_error()
     assert lib.tq_lstm_cell_f32(None, None, None, None, -1, 3, None) == 1
     assert lib.tq_lstm_cell_f32(None, None, None, None, 0, 3, None) == 0  # nothing to do
+
+
+def test_swish_epilogue_and_act_encode_act_validation():
+    """relu 3 (swish, EfficientNet) is accepted by the fp16 entry for the direct engine's
+    shapes only, never by the VALU entry; tq_act_encode_act validates act and sf."""
+    lib = tq_native.lib()
+    out = ctypes.c_void_p(16)
+    epi = tq_native.ConvEpilogue()
+    epi.relu = 4
+    rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 64, None, 64, 1, 1, 64, 1, 1, 0, 0, 1, 1,
+                                    1.0, None, out, 8, 8, 1, 0, -1, ctypes.byref(epi), None)
+    assert rc == 1 and b"relu" in lib.tq_last_error()
+    epi.relu = 3
+    rc = lib.tq_conv2d_termpair_f16(None, 1, 8, 8, 16, None, 64, 3, 3, 192, 1, 1, 1, 1, 1, 1,
+                                    1.0, None, out, 8, 8, 1, 0, -1, ctypes.byref(epi), None)
+    assert rc == 2 and b"swish" in lib.tq_last_error()
+    rc = lib.tq_conv2d_termpair_fused(None, 1, 8, 8, 64, None, 64, 1, 1, 64, 1, 1, 0, 0, 1, 1,
+                                      1.0, None, out, 8, 8, ctypes.byref(epi), None)
+    assert rc == 2 and b"swish" in lib.tq_last_error()
+    buf = ctypes.c_void_p(64)
+    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, None, 1, None, 0.1, 9, 3, buf, 8, 1,
+                                 None) == 1
+    assert b"act" in lib.tq_last_error()
+    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, None, 3, None, 0.0, 9, 3, buf, 8, 1,
+                                 None) == 1
+    assert b"sf" in lib.tq_last_error()
+    assert tq_native.act_code("swish") == 3 and tq_native.act_code(6) == 2
