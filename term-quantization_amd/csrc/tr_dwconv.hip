@@ -140,9 +140,7 @@ __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
 // weights are loaded once for kDwRows outputs and every load of a tap row is issued
 // unrolled (no per-tap dependent branch chain).  Lanes run chunk-fastest, then along the
 // output row: a wave's loads of one tap cover contiguous NHWC bytes.
-constexpr int kDwRows = 4;
-
-template <int KH, int KW>
+template <int KH, int KW, int kDwRows>
 __global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
   if (a.lut_c) {
@@ -215,16 +213,20 @@ __global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.N * a.Ho * a.Wo * (a.Cp / 8);
   if (n == 0) return hipSuccess;
-  static const char* rows = getenv("TQ_DW_ROWS");  // A/B override (tools only): 0 off
-  if (!(rows && atoi(rows) == 0) && a.dh == 1 && a.dw == 1 &&
+  // A/B override (tools only): TQ_DW_ROWS=0 the flat kernel, =4 four rows for 5x5 too
+  static const char* rows_env = getenv("TQ_DW_ROWS");
+  if (!(rows_env && atoi(rows_env) == 0) && a.dh == 1 && a.dw == 1 &&
       ((a.KH == 3 && a.KW == 3) || (a.KH == 5 && a.KW == 5))) {
-    const int64_t lanes =
-        (int64_t)a.N * ((a.Ho + kDwRows - 1) / kDwRows) * a.Wo * (a.Cp / 8);
+    // four output rows per lane for 3x3, two for 5x5 (four would need 180 VGPRs)
+    const int rows = a.KH == 3 ? 4 : (rows_env && atoi(rows_env) == 4 ? 4 : 2);
+    const int64_t lanes = (int64_t)a.N * ((a.Ho + rows - 1) / rows) * a.Wo * (a.Cp / 8);
     const dim3 grid((unsigned)((lanes + 255) / 256));
     if (a.KH == 3)
-      dwconv_tp_rows_kernel<3, 3><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
+      dwconv_tp_rows_kernel<3, 3, 4><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
+    else if (rows == 4)
+      dwconv_tp_rows_kernel<5, 5, 4><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
     else
-      dwconv_tp_rows_kernel<5, 5><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
+      dwconv_tp_rows_kernel<5, 5, 2><<<grid, 256, (size_t)a.lut_c * 2, stream>>>(a);
     return hipGetLastError();
   }
   dwconv_tp_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, (size_t)a.lut_c * 2, stream>>>(a);
