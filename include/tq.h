@@ -82,18 +82,22 @@ int tq_act_encode(const float *x, int32_t in_nhwc, int64_t n, int64_t c, int64_t
                   int64_t cp, int32_t fmt, void *stream);
 
 /*
- * Activation / squeeze-excite gate + activation TR of EfficientNet-b0's MBConv tensors
+ * Affine / activation / squeeze-excite gate + activation TR of MobileNet-V2's and
+ * EfficientNet-b0's stem and MBConv tensors
  * (efficientnet_pytorch MBConvBlock.forward: swish(bn0(expand_conv(x))), and
  * x = torch.sigmoid(x_sq) * x before the project conv; the consumer's input TR,
  * tr_layer.py:96-99), channels_last:
- *   v = x[p][c], or swish(v) = v * sigmoid(v) if act == 3 (act 0: none)
+ *   v = x[p][c]; v = fp32 fma(v, ch_scale[c], ch_shift[c]) (if ch_scale: an eval BatchNorm
+ *   as a per-channel affine, e.g. a stem's bn0); v = act(v): 0 none, 1 ReLU, 2 ReLU6,
+ *   3 swish v * sigmoid(v)
  *   out[p][c] = v                       (if out: the fp32 activation)
  *   v = fp32(gate[img][c] * v)          (if gate: the squeeze-excite sigmoid, [n][c] fp32)
  *   codes[p][c] = TR(v; sf, bitwidth, num_keep_terms)   [n][h][w][cp] as tq_act_encode
  * x, out: [n][h][w][c] fp32, 16-byte aligned; 0 < sf < inf.
  */
 int tq_act_encode_act(const float *x, int64_t n, int64_t c, int64_t h, int64_t w,
-                      const float *gate, int32_t act, float *out, float sf, int32_t bitwidth,
+                      const float *ch_scale, const float *ch_shift, const float *gate,
+                      int32_t act, float *out, float sf, int32_t bitwidth,
                       int32_t num_keep_terms, void *codes, int64_t cp, int32_t fmt,
                       void *stream);
 

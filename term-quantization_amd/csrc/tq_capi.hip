@@ -124,15 +124,19 @@ int tq_act_encode(const float* x, int32_t in_nhwc, int64_t n, int64_t c, int64_t
 }
 
 int tq_act_encode_act(const float* x, int64_t n, int64_t c, int64_t h, int64_t w,
-                      const float* gate, int32_t act, float* out, float sf, int32_t bitwidth,
+                      const float* ch_scale, const float* ch_shift, const float* gate,
+                      int32_t act, float* out, float sf, int32_t bitwidth,
                       int32_t num_keep_terms, void* codes, int64_t cp, int32_t fmt,
                       void* stream) {
   if (n < 0 || c < 1 || h < 0 || w < 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: bad shape");
   if (x == nullptr || codes == nullptr)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: null buffer");
-  if (act != 0 && act != tq::kActSwish)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: act must be 0 (none) or 3 (swish)");
+  if (act < 0 || act > tq::kActSwish)
+    return fail(TQ_ERR_INVALID_ARGUMENT,
+                "act_encode_act: act must be 0 (none), 1 (ReLU), 2 (ReLU6) or 3 (swish)");
+  if ((ch_scale == nullptr) != (ch_shift == nullptr))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: ch_scale and ch_shift go together");
   if (cp < c || cp % 8 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: cp must be >= c and a multiple of 8");
   if (fmt != TQ_CODES_I16 && fmt != TQ_CODES_F16)
@@ -145,7 +149,8 @@ int tq_act_encode_act(const float* x, int64_t n, int64_t c, int64_t h, int64_t w
   if ((uintptr_t)codes % 16 != 0 || (uintptr_t)x % 16 != 0 || (uintptr_t)out % 16 != 0)
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: x, out, codes must be 16-byte aligned");
   const int kk = num_keep_terms < 0 ? 0 : num_keep_terms;
-  return hip_status(tq::launch_act_encode_act(x, gate, act, out, n, c, h, w, sf, bitwidth, kk,
+  return hip_status(tq::launch_act_encode_act(x, ch_scale, ch_shift, gate, act, out, n, c, h,
+                                              w, sf, bitwidth, kk,
                                               static_cast<int16_t*>(codes), cp, fmt,
                                               (hipStream_t)stream),
                     "act_encode_act launch");

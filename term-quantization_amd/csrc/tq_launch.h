@@ -130,7 +130,8 @@ struct PoolArgs {
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream);
 
-hipError_t launch_act_encode_act(const float* x, const float* gate, int act, float* out,
+hipError_t launch_act_encode_act(const float* x, const float* ch_scale, const float* ch_shift,
+                                 const float* gate, int act, float* out,
                                  int64_t N, int64_t C, int64_t H, int64_t W, float sf,
                                  int bitwidth, int k, int16_t* codes, int64_t Cp, int fmt,
                                  hipStream_t stream);

@@ -422,7 +422,9 @@ __global__ __launch_bounds__(256) void act_encode_kernel(const float* __restrict
 // out: the fp32 activation), v = fp32(gate[img][c] * v) (if gate: MBConvBlock.forward's
 // x = sigmoid(x_sq) * x), codes[p][c] = TR(v) for the next conv (pad channels zero).
 __global__ __launch_bounds__(256) void act_encode_act_kernel(
-    const float* __restrict__ x, const float* __restrict__ gate, int act, float* __restrict__ out,
+    const float* __restrict__ x, const float* __restrict__ ch_scale,
+    const float* __restrict__ ch_shift, const float* __restrict__ gate, int act,
+    float* __restrict__ out,
     int16_t* __restrict__ codes, int64_t npix, int64_t HW, int C, int Cp, double inv_sf,
     float maxv, int k, int fmt) {
   const int chunks = Cp / 8;
@@ -441,6 +443,11 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? x[pix * C + c0 + i] : 0.0f;
+  }
+  if (ch_scale) {  // eval BatchNorm as a per-channel fp32 affine (a stem's bn before its act)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      v[i] = c0 + i < C ? fmaf(v[i], ch_scale[c0 + i], ch_shift[c0 + i]) : 0.0f;
   }
   float o[8];
 #pragma unroll
@@ -469,7 +476,8 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
 
 }  // namespace
 
-hipError_t launch_act_encode_act(const float* x, const float* gate, int act, float* out,
+hipError_t launch_act_encode_act(const float* x, const float* ch_scale, const float* ch_shift,
+                                 const float* gate, int act, float* out,
                                  int64_t N, int64_t C, int64_t H, int64_t W, float sf,
                                  int bitwidth, int k, int16_t* codes, int64_t Cp, int fmt,
                                  hipStream_t stream) {
@@ -478,7 +486,8 @@ hipError_t launch_act_encode_act(const float* x, const float* gate, int act, flo
   const int64_t n = npix * (Cp / 8);
   if (n == 0) return hipSuccess;
   act_encode_act_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
-      x, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, 1.0 / (double)sf, maxv, k, fmt);
+      x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp,
+      1.0 / (double)sf, maxv, k, fmt);
   return hipGetLastError();
 }
 

@@ -27,6 +27,14 @@ import tq_ops
 import tr_layer
 
 
+def _bn_affine(bn):
+    """An eval BatchNorm as an fp32 per-channel affine (scale, shift) for tq_act_encode_act."""
+    a = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    return (a.float().contiguous(),
+            (bn.bias.detach().double() - bn.running_mean.detach().double() * a).float()
+            .contiguous())
+
+
 def _fold_bn(layer, bn):
     """Per-channel (scale, shift) in fp64: bn(acc * s + bias) == acc * scale + shift."""
     dev = layer.w_codes.device
@@ -467,6 +475,11 @@ class FusedMobileNetV2(nn.Module):
             raise ValueError("not a torchvision-style MobileNet-V2")
         last = feats[-1]
         self.last = _Conv(last[0], last[1], nonneg=False)
+        # stem: torch conv, then BN + ReLU6 + the first block's codes in one pass
+        self.stem_affine = None
+        if (len(self.stem) == 3 and isinstance(self.stem[1], nn.BatchNorm2d) and
+                isinstance(self.stem[2], nn.ReLU6) and not self.stem[1].training):
+            self.stem_affine = _bn_affine(self.stem[1])
 
     @torch.no_grad()
     def forward(self, x, capture=None):
@@ -476,12 +489,24 @@ class FusedMobileNetV2(nn.Module):
         m = self.qmodel
         keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
-        y0 = self.stem(x).contiguous(memory_format=torch.channels_last)  # conv, BN, ReLU6
         first = self.blocks[0].first_consumer()
-        codes = torch.empty((y0.shape[0], y0.shape[2], y0.shape[3], first.cp_in),
-                            dtype=first.code_dtype, device=x.device)
-        tq_ops._launch("act_encode", 4 * y0.numel() + 2 * codes.numel(),
-                       lambda: tq_native.act_encode(y0, True, *first.quant, codes))
+        if self.stem_affine is not None:
+            z = self.stem[0](x).contiguous(memory_format=torch.channels_last)
+            codes = torch.empty((z.shape[0], z.shape[2], z.shape[3], first.cp_in),
+                                dtype=first.code_dtype, device=x.device)
+            y0 = torch.empty_like(z) if (keep or self.blocks[0].use_res) else None
+            tq_ops._launch("act_encode_act", 4 * z.numel() + 2 * codes.numel(),
+                           lambda: tq_native.act_encode_act(z, *first.quant, codes, act=6,
+                                                            out=y0, affine=self.stem_affine))
+        else:
+            y0 = self.stem(x).contiguous(memory_format=torch.channels_last)  # conv, BN, ReLU6
+            codes = torch.empty((y0.shape[0], y0.shape[2], y0.shape[3], first.cp_in),
+                                dtype=first.code_dtype, device=x.device)
+            tq_ops._launch("act_encode", 4 * y0.numel() + 2 * codes.numel(),
+                           lambda: tq_native.act_encode(y0, True, *first.quant, codes))
+        if keep:
+            capture.append({"name": "stem", "kind": "stem", "out": y0, "codes_out": codes,
+                            "quant": first.quant})
         xin = y0
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
@@ -587,6 +612,8 @@ class FusedEfficientNet(nn.Module):
             raise ValueError("not an efficientnet_pytorch-style EfficientNet")
         self.blocks = [_MBConv(b) for b in qmodel._blocks]
         self.head = _Conv(qmodel._conv_head, qmodel._bn1, nonneg=False)
+        # stem: torch conv, then BN + swish + the first block's codes in one pass
+        self.stem_affine = None if qmodel._bn0.training else _bn_affine(qmodel._bn0)
 
     @torch.no_grad()
     def forward(self, x, capture=None):
@@ -596,12 +623,26 @@ class FusedEfficientNet(nn.Module):
         m = self.qmodel
         keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
-        y0 = m._swish(m._bn0(m._conv_stem(x))).contiguous(memory_format=torch.channels_last)
         first = self.blocks[0].first_consumer()
-        codes = torch.empty((y0.shape[0], y0.shape[2], y0.shape[3], first.cp_in),
-                            dtype=first.code_dtype, device=x.device)
-        tq_ops._launch("act_encode", 4 * y0.numel() + 2 * codes.numel(),
-                       lambda: tq_native.act_encode(y0, True, *first.quant, codes))
+        if self.stem_affine is not None:
+            z = m._conv_stem(x).contiguous(memory_format=torch.channels_last)
+            codes = torch.empty((z.shape[0], z.shape[2], z.shape[3], first.cp_in),
+                                dtype=first.code_dtype, device=x.device)
+            y0 = torch.empty_like(z) if (keep or self.blocks[0].use_res) else None
+            tq_ops._launch("act_encode_act", 4 * z.numel() + 2 * codes.numel(),
+                           lambda: tq_native.act_encode_act(z, *first.quant, codes,
+                                                            act="swish", out=y0,
+                                                            affine=self.stem_affine))
+        else:
+            y0 = m._swish(m._bn0(m._conv_stem(x))).contiguous(
+                memory_format=torch.channels_last)
+            codes = torch.empty((y0.shape[0], y0.shape[2], y0.shape[3], first.cp_in),
+                                dtype=first.code_dtype, device=x.device)
+            tq_ops._launch("act_encode", 4 * y0.numel() + 2 * codes.numel(),
+                           lambda: tq_native.act_encode(y0, True, *first.quant, codes))
+        if keep:
+            capture.append({"name": "stem", "kind": "stem", "out": y0, "codes_out": codes,
+                            "quant": first.quant})
         xin = y0
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None

@@ -39,8 +39,8 @@ _SIGNATURES = {
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
                          _vp],
-    "tq_act_encode_act": [_vp, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _f32, _i32, _i32, _vp,
-                          _i64, _i32, _vp],
+    "tq_act_encode_act": [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _vp, _f32, _i32,
+                          _i32, _vp, _i64, _i32, _vp],
     "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _i32,
                       _vp],
     "tq_conv2d_cout_align": [],
@@ -272,10 +272,12 @@ def act_code(relu):
     return 2 if relu == 6 else int(bool(relu))
 
 
-def act_encode_act(x, sf, bitwidth, num_keep_terms, codes, act=None, gate=None, out=None):
-    """codes = TR(gate[n, c] * act(x)) (tq_act_encode_act): x fp32 channels_last [N, C, H, W],
-    act None or "swish", gate None or fp32 [N, C] (EfficientNet's squeeze-excite sigmoid),
-    ``out`` (optional, channels_last like x) receives act(x)."""
+def act_encode_act(x, sf, bitwidth, num_keep_terms, codes, act=None, gate=None, out=None,
+                   affine=None):
+    """codes = TR(gate[n, c] * act(x * scale[c] + shift[c])) (tq_act_encode_act): x fp32
+    channels_last [N, C, H, W], ``affine`` None or fp32 (scale, shift) [C] (an eval BN), act
+    None / True / 6 / "swish", gate None or fp32 [N, C] (EfficientNet's squeeze-excite
+    sigmoid), ``out`` (optional, channels_last like x) receives act(affine(x))."""
     n, c, h, w = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise RuntimeError("act_encode_act: x must be channels_last")
@@ -286,7 +288,9 @@ def act_encode_act(x, sf, bitwidth, num_keep_terms, codes, act=None, gate=None, 
                             not out.is_contiguous(memory_format=torch.channels_last)):
         raise RuntimeError("act_encode_act: out must be channels_last like x")
     with torch.cuda.device(x.device):
-        rc = lib().tq_act_encode_act(_ptr(x), n, c, h, w, _ptr(gate), act_code(act), _ptr(out),
+        sc, sh = affine if affine is not None else (None, None)
+        rc = lib().tq_act_encode_act(_ptr(x), n, c, h, w, _ptr(sc), _ptr(sh), _ptr(gate),
+                                     act_code(act), _ptr(out),
                                      sf, bitwidth, num_keep_terms, _ptr(codes), codes.shape[-1],
                                      code_format(codes), _stream(x))
     _check(rc)

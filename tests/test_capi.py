@@ -179,10 +179,13 @@ def test_swish_epilogue_and_act_encode_act_validation():
                                       1.0, None, out, 8, 8, ctypes.byref(epi), None)
     assert rc == 2 and b"swish" in lib.tq_last_error()
     buf = ctypes.c_void_p(64)
-    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, None, 1, None, 0.1, 9, 3, buf, 8, 1,
-                                 None) == 1
+    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, None, None, None, 4, None, 0.1, 9, 3, buf,
+                                 8, 1, None) == 1
     assert b"act" in lib.tq_last_error()
-    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, None, 3, None, 0.0, 9, 3, buf, 8, 1,
-                                 None) == 1
+    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, buf, None, None, 2, None, 0.1, 9, 3, buf,
+                                 8, 1, None) == 1
+    assert b"together" in lib.tq_last_error()
+    assert lib.tq_act_encode_act(buf, 1, 8, 2, 2, None, None, None, 3, None, 0.0, 9, 3, buf,
+                                 8, 1, None) == 1
     assert b"sf" in lib.tq_last_error()
     assert tq_native.act_code("swish") == 3 and tq_native.act_code(6) == 2

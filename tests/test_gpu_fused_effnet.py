@@ -70,10 +70,27 @@ def net():
 
 def _consumer_quant(cap, codes):
     for cand in cap:
-        if cand["codes_in"] is codes:
+        if cand.get("codes_in") is codes:
             cc = cand["conv"]
             return cc.consumer.quant if cand["kind"] == "dw" else cc.quant
     return None
+
+
+def _check_stem(q, x, rec, module_stem):
+    """The stem's fused BN + activation + encode pass (tq_act_encode_act): its fp32 output
+    within 1e-5 of the module stem (torch BN + activation), its codes bit-exact TR of it."""
+    assert rec["kind"] == "stem"
+    with torch.no_grad():
+        ref = module_stem().double().cpu()
+    y = rec["out"].double().cpu()
+    scale = ref.abs().amax(dim=(0, 2, 3), keepdim=True) + 1e-30
+    assert bool(((y - ref).abs() <= 1e-5 * scale).all())
+    sf, db, dt = rec["quant"]
+    c = y.shape[1]
+    yq = oracle.tr(y.float().numpy().reshape(1, -1, 1, 1), sf, db, 1, dt)
+    exp = torch.from_numpy(np.rint(yq.reshape(y.shape) / np.float32(sf)).astype(np.int64))
+    got = rec["codes_out"][..., :c].long().cpu().permute(0, 3, 1, 2)
+    assert torch.equal(got, exp)
 
 
 def test_fused_efficientnet_b0_teacher_forced(net):
@@ -84,8 +101,9 @@ def test_fused_efficientnet_b0_teacher_forced(net):
     logits = fused(x)
     torch.cuda.synchronize()
     assert torch.equal(logits, logits_cap)
-    assert len(cap) == 16 + 16 + 15 + 1  # dw + project per block, 15 expand convs, the head
-    for rec in cap:
+    assert len(cap) == 1 + 16 + 16 + 15 + 1  # stem, dw + project per block, 15 expand, head
+    _check_stem(q, x, cap[0], lambda: q._swish(q._bn0(q._conv_stem(x))))
+    for rec in cap[1:]:
         conv = rec["conv"]
         layer = conv.layer
         sf = (conv.consumer.quant if rec["kind"] == "dw" else conv.quant)[0]

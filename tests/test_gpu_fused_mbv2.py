@@ -56,6 +56,23 @@ def net():
     return q, x
 
 
+def _check_stem(q, x, rec, module_stem):
+    """The stem's fused BN + activation + encode pass (tq_act_encode_act): its fp32 output
+    within 1e-5 of the module stem (torch BN + activation), its codes bit-exact TR of it."""
+    assert rec["kind"] == "stem"
+    with torch.no_grad():
+        ref = module_stem().double().cpu()
+    y = rec["out"].double().cpu()
+    scale = ref.abs().amax(dim=(0, 2, 3), keepdim=True) + 1e-30
+    assert bool(((y - ref).abs() <= 1e-5 * scale).all())
+    sf, db, dt = rec["quant"]
+    c = y.shape[1]
+    yq = oracle.tr(y.float().numpy().reshape(1, -1, 1, 1), sf, db, 1, dt)
+    exp = torch.from_numpy(np.rint(yq.reshape(y.shape) / np.float32(sf)).astype(np.int64))
+    got = rec["codes_out"][..., :c].long().cpu().permute(0, 3, 1, 2)
+    assert torch.equal(got, exp)
+
+
 def test_fused_mobilenet_v2_teacher_forced(net):
     q, x = net
     fused = tq_fuse.FusedMobileNetV2(q)
@@ -63,8 +80,9 @@ def test_fused_mobilenet_v2_teacher_forced(net):
     logits_cap = fused(x, capture=cap)
     logits = fused(x)
     assert torch.equal(logits, logits_cap)
-    assert len(cap) == 2 * 17 + 16 + 1  # 17 dw + 17 project + 16 expand + the last conv
-    for rec in cap:
+    assert len(cap) == 1 + 2 * 17 + 16 + 1  # stem, 17 dw + 17 project + 16 expand, last
+    _check_stem(q, x, cap[0], lambda: q.features[0](x))
+    for rec in cap[1:]:
         conv = rec["conv"]
         layer = conv.layer
         sf, db, dt = conv.consumer.quant if rec["kind"] == "dw" else conv.quant
@@ -96,7 +114,7 @@ def test_fused_mobilenet_v2_teacher_forced(net):
         if rec["codes_out"] is not None:
             nxt_quant = None
             for cand in cap:
-                if cand["codes_in"] is rec["codes_out"]:
+                if cand.get("codes_in") is rec["codes_out"]:
                     cc = cand["conv"]
                     nxt_quant = cc.consumer.quant if cand["kind"] == "dw" else cc.quant
             assert nxt_quant is not None, rec["name"]
