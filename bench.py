@@ -72,6 +72,11 @@ def parse():
                          "HIP stream each, launches issued layer by layer round-robin (2: "
                          "each kernel's drain overlaps the other chunk's kernel; 1 = one "
                          "stream)")
+    ap.add_argument("--no-d1", action="store_true",
+                    help="skip the d1_tr_op key (SURVEY 8(d) D1: the TR op alone)")
+    ap.add_argument("--no-d4", action="store_true",
+                    help="skip the d4 key (BASELINE configs[2]/[3]: LSTM-650, fused "
+                         "MobileNet-V2 / EfficientNet-b0; rank 0 at N=1 only)")
     ap.add_argument("--unfused", action="store_true",
                     help="run the module path (separate BN/ReLU/add/TR passes) instead of "
                          "the fused executor")
@@ -275,6 +280,34 @@ def cpu_tr_op_baseline(oracle, n=1 << 24):
             "product_host_tr_elements_per_s": host}
 
 
+def d1_tr_op(dev, iters=20):
+    """the TR op alone on the ResNet-18 layer-1 activation tensor,
+    relu(N(0,1)) 256x64x56x56 fp32 (seed 0), sf=0.05, db=9, dt=3, g=1, viewed (1,-1,1,1) as
+    tr_layer.py:96-99 calls it; 8 algorithmic bytes per element (fp32 read + write), HIP
+    events on the launch stream, against the 8 TB/s HBM peak."""
+    import tq_native
+    torch.manual_seed(0)
+    x = torch.relu(torch.randn(256, 64, 56, 56, device=dev)).view(1, -1, 1, 1)
+    out = torch.empty_like(x)
+    run = lambda: tq_native.tr_into(x, out, 0.05, DB, 1, DT)  # noqa: E731
+    for _ in range(3):
+        run()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(iters):
+        run()
+    b.record(s)
+    torch.cuda.synchronize()
+    t = a.elapsed_time(b) * 1e-3 / iters
+    n = x.numel()
+    gbs = 8 * n / t / 1e9
+    return {"kernel": "tr_elem_kernel<float> (g=1: quantize + closed-form HESE + keep dt terms "
+                      "+ rescale)", "elements": n, "us_per_launch": t * 1e6,
+            "elements_per_s": n / t, "achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
+            "hbm_frac": gbs / HBM_PEAK_GBS, "bytes_per_element": 8, "launches": iters}
+
+
 def main():
     args = parse()
     os.environ["TQ_CONV_ENGINE"] = args.engine
@@ -361,10 +394,14 @@ def main():
         # kernel -- the timed region's overlap is an executor-level gain, reported in value).
         timer = KernelTimer()
         tq_ops.set_kernel_hook(timer)
+        pass_end = torch.cuda.Event(enable_timing=True)
         for i in range(args.steps):
             runner(batches[i % 2][0])
+        pass_end.record(torch.cuda.current_stream())
         torch.cuda.synchronize()
         tq_ops.set_kernel_hook(None)
+        # GPU time of that one-stream pass (its kernels plus the event gaps between them)
+        roof_pass_s = timer.base.elapsed_time(pass_end) * 1e-3
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -427,7 +464,10 @@ def main():
             "avg_launch_us": conv["seconds"] / conv["launches"] * 1e6,
             "busy_us_per_launch": conv_t * 1e6,
             "launches": conv["launches"],
-            "share_of_step": conv["busy"] / elapsed,
+            # like for like: the convs' busy time over the GPU time of the same one-stream
+            # roofline pass (both include the ~10 us event gaps' absence / presence alike)
+            "share_of_roofline_pass": conv["busy"] / roof_pass_s,
+            "roofline_pass_ms_per_step": roof_pass_s / args.steps * 1e3,
             # the north star's HBM roofline of the whole path: 15,026,432
             # algorithmic bytes per image (fp32 TR-layer inputs + outputs + weights/256) at
             # the measured images/s against the 8 TB/s HBM peak
@@ -487,7 +527,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f16" if mfma else "int16",
+            # exact integer term-pair sums: codes are integers held in fp16 (MFMA engine) or
+            # int16 (VALU engine), products exact in fp32, sums flushed to int32
+            "dtype": "int (exact, fp16-coded)" if mfma else "int (exact, int16-coded)",
             "data": "synthetic",
             "config": {"workload": "resnet18-tq-g8-k12 (wb=db=9, dt=3), synthetic N(0,1) "
                                    "3x224x224, random-init weights",
@@ -497,13 +539,23 @@ def main():
                        "executor": "module path" if args.unfused else
                                    "fused (BN/ReLU/residual/next-layer TR in the conv "
                                    "epilogue)",
-                       "launch": launch, "streams": args.streams},
+                       "launch": launch, "streams": args.streams,
+                       # the stem conv (not a TR layer; fp32 torch in the reference) runs in
+                       # the fused stem kernel as a split-fp16 near-fp32 conv
+                       "stem": "split-fp16 near-fp32 (fused stem kernel)"
+                               if enc_name == "stem_conv_pool" else "torch fp32 conv"},
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,
             "roofline": roof,
             "roofline_tr": roof_tr,
             "accuracy_counters": acc_counters,
         }
+        if world == 1 and not args.no_d1:
+            result["d1_tr_op"] = d1_tr_op(dev)
+        if world == 1 and not args.no_d4:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import bench_d4
+            result["d4"] = bench_d4.d4_summary(dev)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(model_fp, qmodel, args.cpu_sample)
     if world > 1:

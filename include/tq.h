@@ -42,6 +42,14 @@ const char *tq_version(void);
 const char *tq_last_error(void);
 
 /*
+ * Diagnostics: the number of bounded team-sync waits of the row-strip conv engine that ran
+ * out since the previous call (each one means a launch went on without confirming that its
+ * LDS patch was staged, so its results are suspect), then clears the count.  Synchronous
+ * (waits for the device); `count` is a host pointer.  A healthy run reads 0.
+ */
+int tq_strip_sync_faults(uint32_t *count);
+
+/*
  * Term-revealing op, float32 / float64.  Replaces the pybind entry
  *   at::Tensor tr(const at::Tensor input, const float sf, const int32_t bitwidth,
  *                 const int32_t group_size, const int32_t num_keep_terms)

@@ -78,6 +78,11 @@ const char* tq_version(void) { return "tq-hip 0.1.0 gfx950"; }
 
 const char* tq_last_error(void) { return g_err; }
 
+int tq_strip_sync_faults(uint32_t* count) {
+  if (count == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "strip_sync_faults: count is null");
+  return hip_status(tq::strip_sync_faults(count), "strip_sync_faults");
+}
+
 int tq_tr_f32(const float* input, float* output, int64_t ndim, const int64_t* shape, float sf,
               int32_t bitwidth, int32_t group_size, int32_t num_keep_terms, void* stream) {
   return tr_impl<float>(input, output, nullptr, ndim, shape, sf, bitwidth, group_size,
@@ -221,9 +226,11 @@ int conv_common(const int16_t* act_codes, int64_t n, int64_t h, int64_t w, int64
 int code_target(const void* codes, int64_t cp, float sf, int32_t bits, int32_t terms,
                 int32_t fmt, int64_t cout, const char* which) {
   if (codes == nullptr) return TQ_OK;
-  if (cp < cout || cp % 8 != 0 || (uintptr_t)codes % 8 != 0)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d epilogue: codes_%s needs cp >= cout, "
-                "cp %% 8 == 0 and 8-byte alignment", which);
+  // the epilogue zeroes the pad channels [cout, cp) only up to the next multiple of 8
+  // (tq_epilogue.h store_codes4), so a wider code row would keep stale pad codes
+  if (cp != (cout + 7) / 8 * 8 || (uintptr_t)codes % 8 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d epilogue: codes_%s needs cp == roundup(cout, "
+                "8) and 8-byte alignment", which);
   if (fmt != TQ_CODES_I16 && fmt != TQ_CODES_F16)
     return fail(TQ_ERR_INVALID_ARGUMENT, "codes_%s: unknown code format %d", which, fmt);
   if (bits < 0 || bits > max_code_bits(fmt))
@@ -490,6 +497,11 @@ int tq_dwconv2d_termpair_fused(const int16_t* act_codes, int64_t n, int64_t h, i
                                int64_t ho, int64_t wo, const tq_dw_epilogue* epi,
                                void* stream) {
   if (epi == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d: epilogue is null");
+  // the fused entry has no scale/bias of its own: its affine is the epilogue's per-channel
+  // (ch_scale, ch_shift) -- without them every output would silently be acc * 0 + 0
+  if (epi->ch_scale == nullptr || epi->ch_shift == nullptr)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "dwconv2d_fused: epilogue ch_scale/ch_shift are "
+                "required");
   return dw_impl(act_codes, n, h, w, c, cp, w_codes, kh, kw, stride_h, stride_w, pad_top,
                  pad_left, dil_h, dil_w, 0.0, nullptr, out, ho, wo, 1, epi, stream);
 }

@@ -171,14 +171,16 @@ __device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
 // TR(NaN) = 0).
 constexpr int kActSwish = 3;
 
-// Four instructions (v_exp_f32 of -y * log2(e), v_rcp_f32) instead of a full-precision expf
-// and an IEEE division: within ~1e-6 (relative) of torch's fp32 swish; the codes are TR of
-// the value stored.  (Used by the depthwise and encode kernels only: a swish branch in the
-// shared term-pair epilogue put the unrolled epilogue arrays of the strip and register-
-// staged engines into scratch, so EfficientNet's 1x1 convs store BN output and
-// tq_act_encode_act applies the swish.)
+// torch's own fp32 composition, operation for operation: sigmoid as 1 / (1 + expf(-y)) with
+// the device library's full-precision expf and an IEEE division (torch's sigmoid kernel),
+// then y * sigmoid(y) (MemoryEfficientSwish), so the stored value -- and the codes, TR of
+// it -- are the module path's bit for bit (tests/test_gpu_fused_effnet.py).  (Used by the
+// depthwise and encode kernels and the direct engine's SWISH instantiation only: a swish
+// branch in the shared term-pair epilogue put the unrolled epilogue arrays of the strip and
+// register-staged engines into scratch.)
 __device__ __forceinline__ float swish_f32(float y) {
-  return y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y * -1.44269504f));
+  const float s = 1.0f / (1.0f + expf(-y));
+  return y * s;
 }
 
 __device__ __forceinline__ void act_apply(int act, float& y, float& o) {

@@ -168,5 +168,7 @@ hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream);
 // W % 8 == 0, W <= 56, kc_steps == 0, NHWC out (ResNet-18 layer 1).
 bool conv_strip_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_strip(const ConvArgs& a, hipStream_t stream);
+// reads and clears the strip engine's team-sync fault counter (synchronous)
+hipError_t strip_sync_faults(uint32_t* count);
 
 }  // namespace tq

@@ -60,6 +60,10 @@ __host__ __device__ inline int64_t strip_lds_bytes(int64_t w) {
   return ((int64_t)kStripWUnits + 2 * strip_patch_px((int)w) * 8 + 64) * 16 + 16;
 }
 
+// Team-sync guard exhaustions since the last tq_strip_sync_faults() (device-wide; a
+// non-zero count means some launch computed with a patch whose staging was not confirmed).
+__device__ uint32_t g_strip_sync_faults;
+
 // Wave-uniform team barrier through an LDS counter: every wave of the team adds 1, then
 // waits until the counter reaches `target` (4 per barrier).  The caller has already retired
 // what the others must see (vmcnt for its LDS-DMA, lgkmcnt for its LDS reads).  The spin is
@@ -71,10 +75,15 @@ __device__ __forceinline__ void team_sync(uint32_t* ctr, uint32_t target) {
 #endif
   if ((threadIdx.x & 63) == 0)
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (int guard = 0; guard < (1 << 22); ++guard) {
+  int guard = 0;
+  for (; guard < (1 << 22); ++guard) {
     if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
     __builtin_amdgcn_s_sleep(1);
   }
+  // guard exhausted: the protocol broke and this wave goes on with a patch that may be
+  // partly staged -- count it where the host can see it (tq_strip_sync_faults)
+  if (guard == (1 << 22) && (threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(&g_strip_sync_faults, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Per-lane epilogue constants.
@@ -449,6 +458,13 @@ hipError_t launch_strip_mode(const ConvArgs& a, hipStream_t stream) {
   conv2d_tp_strip_kernel<RES, OUT, CB><<<dim3((unsigned)grid), kStripThreads, (size_t)bytes,
                                           stream>>>(b, ntiles);
   return hipGetLastError();
+}
+
+hipError_t strip_sync_faults(uint32_t* count) {
+  uint32_t zero = 0;
+  hipError_t e = hipMemcpyFromSymbol(count, HIP_SYMBOL(g_strip_sync_faults), sizeof(uint32_t));
+  if (e != hipSuccess) return e;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_strip_sync_faults), &zero, sizeof(uint32_t));
 }
 
 hipError_t launch_conv2d_strip(const ConvArgs& a, hipStream_t stream) {

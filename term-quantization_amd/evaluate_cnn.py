@@ -38,7 +38,9 @@ def _rank():
 
 
 def eval_model(args, model, weight_bits, group_size, weight_terms, data_bits, data_terms):
-    """Convert, count term-pair MACs, calibrate, evaluate (evaluate_cnn.py:20-42)."""
+    """Convert, count term-pair MACs, calibrate, evaluate (evaluate_cnn.py:20-42).  The
+    calibration pass sees pct=0.05 of the set, i.e. the same global batches at any world
+    size; the histograms are summed over ranks before the scale-factor search."""
     tr_params = cnn_models.static_conv_layer_settings(model, weight_bits,
                                                       group_size, weight_terms)
     avg_terms = compute_avg_terms(tr_params)
@@ -76,13 +78,17 @@ def build_parser(description='PyTorch ImageNet Training'):
                         metavar='N', help='mini-batch size (default: 256)')
     parser.add_argument('-p', '--print-freq', default=10, type=int,
                         metavar='N', help='print frequency (default: 10)')
-    parser.add_argument('--gpu', default=None, type=int, help='GPU id to use.')
+    parser.add_argument('--gpu', default=None, type=int,
+                        help='GPU id to use (-1: run on the CPU, gloo between ranks).')
     parser.add_argument('-v', '--verbose', action='store_true', help='verbose flag')
     # additions: offline operation and output location
     parser.add_argument('--synthetic', action='store_true',
                         help='synthetic N(0,1) images + random-init weights (no dataset)')
     parser.add_argument('--num-samples', default=1024, type=int,
                         help='synthetic validation set size')
+    parser.add_argument('--image-size', default=224, type=int,
+                        help='synthetic image size (the term-pair MAC count is always taken '
+                             'at 224x224, evaluate_cnn.py:28-29)')
     parser.add_argument('--seed', default=0, type=int)
     parser.add_argument('--out-dir', default='results')
     parser.add_argument('--channels-last', action='store_true',
@@ -91,28 +97,44 @@ def build_parser(description='PyTorch ImageNet Training'):
 
 
 def setup(args):
-    """Device, process group, loader, criterion and the fp32 model."""
+    """Device, process group, loader, criterion and the fp32 model.
+
+    One process per device under torchrun: RCCL ("nccl") on GPUs, gloo on the CPU
+    (``--gpu -1``, or no GPU present).  Every rank evaluates its own strided share of the
+    batches -- the synthetic set and the ImageFolder alike (util.StridedBatchSampler) -- so
+    the all-reduced counters cover each sample exactly once."""
     global val_loader, criterion
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if world > 1:
-        args.gpu = int(os.environ.get('LOCAL_RANK', '0'))
-        torch.cuda.set_device(args.gpu)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', args.gpu))
-    if args.gpu is None:
-        args.gpu = 0
-    if args.synthetic:
-        val_loader = util.SyntheticImageNet(args.num_samples, args.batch_size, seed=args.seed,
-                                            rank=_rank(), world_size=world)
+    rank = int(os.environ.get('RANK', '0'))
+    use_cpu = (args.gpu is not None and args.gpu < 0) or not torch.cuda.is_available()
+    if use_cpu:
+        args.gpu = None
+        dev = torch.device('cpu')
     else:
-        val_loader = util.get_imagenet_validation(args)
         if world > 1:
-            raise RuntimeError('multi-GPU evaluation of a real dataset: shard the ImageFolder '
-                               'with a DistributedSampler (use --synthetic offline)')
-    criterion = nn.CrossEntropyLoss().cuda(args.gpu)
+            args.gpu = int(os.environ.get('LOCAL_RANK', '0'))
+        if args.gpu is None:
+            args.gpu = 0
+        torch.cuda.set_device(args.gpu)
+        dev = torch.device('cuda', args.gpu)
+    if world > 1:
+        if use_cpu:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=dev)
+    val_loader = util.get_imagenet_validation(args, rank=_rank(), world_size=world)
+    criterion = nn.CrossEntropyLoss().to(dev)
     torch.manual_seed(args.seed)
-    model = cnn_models.__dict__[args.arch](pretrained=not args.synthetic).cuda(args.gpu)
+    model = cnn_models.__dict__[args.arch](pretrained=not args.synthetic).to(dev)
     model.eval()
     return model
+
+
+def finish():
+    """Tear the process group down (torchrun ranks)."""
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def save(args, results, name):
@@ -172,3 +194,4 @@ if __name__ == '__main__':
             results[key]['params'].append(params)
 
     save(args, results, '{}-results.json'.format(args.arch))
+    finish()

@@ -3,13 +3,20 @@ evaluate_group_size.py (evaluate_group_size.py:1-91), same CLI and result JSON.
 
     python evaluate_group_size.py <val_dir> -a resnet18
     torchrun --nproc-per-node 8 evaluate_group_size.py --synthetic -a resnet18
+    torchrun --nproc-per-node 2 evaluate_group_size.py --synthetic -a resnet18 --gpu -1  # CPU
 
-Each of the 25 settings is evaluated batch-sharded over all ranks.
+Each of the 25 settings is evaluated batch-sharded over all ranks; the
+results JSON does not depend on the world size.
 """
+import evaluate_cnn
 from evaluate_cnn import build_parser, eval_model, save, setup
 
-if __name__ == '__main__':
-    args = build_parser().parse_args()
+AVG_TERM_SETTINGS = [1.0, 1.25, 1.5, 2.0, 3.0]
+GROUP_SIZES = [1, 2, 8, 16, 32]
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
     model = setup(args)
 
     results = {}
@@ -19,12 +26,10 @@ if __name__ == '__main__':
     group_size = 8
     data_bits = 9
     data_terms = 3
-    avg_term_settings = [1.0, 1.25, 1.5, 2.0, 3.0]
-    group_sizes = [1, 2, 8, 16, 32]
-    for group_size in group_sizes:
+    for group_size in GROUP_SIZES:
         key = str(group_size)
         results[key] = {'avg_terms': [], 'accs': [], 'tmacs': []}
-        for avg_term in avg_term_settings:
+        for avg_term in AVG_TERM_SETTINGS:
             weight_terms = round(avg_term * group_size)
             res = eval_model(args, model, weight_bits, group_size,
                              weight_terms, data_bits, data_terms)
@@ -35,3 +40,9 @@ if __name__ == '__main__':
             results[key]['avg_terms'].append(avg_term)
 
     save(args, results, '{}-group-size-results.json'.format(args.arch))
+    evaluate_cnn.finish()
+    return results
+
+
+if __name__ == '__main__':
+    main()

@@ -35,6 +35,7 @@ _vp = ctypes.c_void_p
 _SIGNATURES = {
     "tq_version": [],
     "tq_last_error": [],
+    "tq_strip_sync_faults": [ctypes.POINTER(ctypes.c_uint32)],
     "tq_tr_f32": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
@@ -218,6 +219,14 @@ def mse_profile_host(x, hist, sfs, bitwidth, num_keep_terms):
 
 def version():
     return lib().tq_version().decode()
+
+
+def strip_sync_faults():
+    """Row-strip engine team-sync waits that ran out since the last call (then cleared;
+    synchronous): 0 in a healthy run (tq_strip_sync_faults)."""
+    n = ctypes.c_uint32(0)
+    _check(lib().tq_strip_sync_faults(ctypes.byref(n)))
+    return int(n.value)
 
 
 def _check(rc):

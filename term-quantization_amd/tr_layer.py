@@ -396,20 +396,32 @@ class TRLSTMLayer(nn.Module):
             weight_bits <= tq_ops.MAX_CODE_BITS and data_bits <= tq_ops.MAX_CODE_BITS)
 
         # ih_l0, hh_l0 (the reference overwrites self.w_sf: the hh scale remains)
-        for name in ('weight_ih_l0', 'weight_hh_l0'):
+        names = ('weight_ih_l0', 'weight_hh_l0')
+        trd = {}
+        for name in names:
             w = getattr(lstm_layer, name)
-            self.w_sf = _w_sf(w, weight_bits)
+            sf = _w_sf(w, weight_bits)
             if self.termpair:
-                wq, codes = tq_ops.tr_encode(w.detach().contiguous(), self.w_sf, weight_bits,
+                wq, codes = tq_ops.tr_encode(w.detach().contiguous(), sf, weight_bits,
                                              self.group_size, self.num_terms)
+                # int32 accumulator bound of the term-pair GEMM, as TRConv2dLayer /
+                # TRLinearLayer check it: sum_k |v_w| * max|v_x| (|v_x| <= 2^data_bits)
+                if codes.abs().to(torch.int64).sum(1).max().item() << data_bits >= 2**31:
+                    self.termpair = False
+            else:
+                wq, codes = tr_cuda.tr(w, sf, weight_bits, self.group_size,
+                                       self.num_terms), None
+            trd[name] = (sf, wq, codes)
+        for name in names:
+            sf, wq, codes = trd[name]
+            self.w_sf = sf
+            if self.termpair:
                 packed, cp, engine, kc = _pack_termpair(codes[:, :, None, None], data_bits,
                                                         weight_bits)
                 kch = _kc_chunk(packed, engine, data_bits, cp, 1)
                 tag = name[7:9]  # 'ih' / 'hh'
                 self.register_buffer('w_codes_' + tag, packed)
                 setattr(self, '_tp_' + tag, (cp, self.w_sf, kc, kch))
-            else:
-                wq = tr_cuda.tr(w, self.w_sf, weight_bits, self.group_size, self.num_terms)
             setattr(lstm_layer, name, nn.Parameter(wq))
 
         self.lstm = lstm_layer

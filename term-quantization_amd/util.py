@@ -10,13 +10,58 @@ import torch
 import torch.distributed as dist
 
 
-def get_imagenet_validation(args):
+class StridedBatchSampler(object):
+    """Batches of consecutive sample indices [i*bs, (i+1)*bs) for the global batch indices
+    i = rank, rank + world, ... -- the static batch stride of the multi-GPU evaluation
+     applied to a map-style dataset: no padding and no duplicated samples,
+    so the all-reduced counters cover every sample exactly once (unlike a padded
+    DistributedSampler), and the union over ranks is the unsharded loader's batches."""
+
+    def __init__(self, num_samples, batch_size, rank=0, world_size=1):
+        self.num_samples, self.batch_size = int(num_samples), int(batch_size)
+        self.rank, self.world_size = int(rank), int(world_size)
+
+    def __len__(self):
+        nb = (self.num_samples + self.batch_size - 1) // self.batch_size
+        return len(range(self.rank, nb, self.world_size))
+
+    def __iter__(self):
+        nb = (self.num_samples + self.batch_size - 1) // self.batch_size
+        for i in range(self.rank, nb, self.world_size):
+            yield list(range(i * self.batch_size,
+                             min((i + 1) * self.batch_size, self.num_samples)))
+
+
+class ShardedLoader(object):
+    """A DataLoader over one rank's strided batches (StridedBatchSampler) that keeps the
+    attributes validate() relies on: ``dataset`` (``.targets``), ``batch_size``, ``rank``,
+    ``world_size`` and ``len`` = the GLOBAL batch count, as SyntheticImageNet does."""
+
+    def __init__(self, dataset, batch_size, rank=0, world_size=1, **loader_kwargs):
+        import torch.utils.data
+        self.dataset, self.batch_size = dataset, batch_size
+        self.rank, self.world_size = rank, world_size
+        self.sampler = StridedBatchSampler(len(dataset), batch_size, rank, world_size)
+        self.loader = torch.utils.data.DataLoader(dataset, batch_sampler=self.sampler,
+                                                  **loader_kwargs)
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        return iter(self.loader)
+
+
+def get_imagenet_validation(args, rank=0, world_size=1):
     """ImageFolder loader of ``<val_dir>/imagenet/val`` (util.py:11-36).  Needs torchvision
-    and the dataset; with ``args.synthetic`` returns ``SyntheticImageNet`` instead."""
+    and the dataset; with ``args.synthetic`` returns ``SyntheticImageNet`` instead.  Either
+    way, ``rank``/``world_size`` shard it by the static batch stride (StridedBatchSampler)."""
     if getattr(args, 'synthetic', False):
         return SyntheticImageNet(num_samples=getattr(args, 'num_samples', 1024),
                                  batch_size=args.batch_size,
-                                 image_size=224, seed=getattr(args, 'seed', 0))
+                                 image_size=getattr(args, 'image_size', 224),
+                                 seed=getattr(args, 'seed', 0), rank=rank,
+                                 world_size=world_size)
     try:
         import PIL
         import torchvision.datasets as datasets
@@ -33,9 +78,9 @@ def get_imagenet_validation(args):
         val_transforms = transforms.Compose([
             transforms.Resize(256), transforms.CenterCrop(224), transforms.ToTensor(),
             normalize])
-    return torch.utils.data.DataLoader(
+    return ShardedLoader(
         datasets.ImageFolder(os.path.join(args.val_dir, 'imagenet', 'val'), val_transforms),
-        batch_size=args.batch_size, shuffle=False, num_workers=args.workers, pin_memory=True)
+        args.batch_size, rank, world_size, num_workers=args.workers, pin_memory=True)
 
 
 class _Targets(object):
@@ -81,45 +126,64 @@ class SyntheticImageNet(object):
 
 def validate(val_loader, model, criterion, args, verbose=True, pct=1.0):
     """Top-1 evaluation loop over (pct of) the loader (util.py:39-80): returns (mean loss,
-    top-1 %) weighted by batch size.  Under torch.distributed the loss / correct / sample
-    sums are all-reduced once at the end, so every rank returns the global figures (the
-    reference reads GPU0's DataParallel gather)."""
+    top-1 %) over the samples seen.  The reference runs batches until the samples seen reach
+    pct of the dataset; here that rule is applied to GLOBAL batch indices, so a loader sharded
+    over ranks (SyntheticImageNet / ShardedLoader: rank r holds batches r, r + world, ...)
+    covers exactly the batches the unsharded loader would.  Under torch.distributed the loss
+    sum and the integer correct / sample counts are all-reduced once at the end, so every rank
+    returns the global figures (the reference reads GPU0's DataParallel gather)."""
     model.eval()
     eval_samples = round(pct * len(val_loader.dataset.targets))
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-    seen = 0
-    totals = [0.0, 0.0, 0.0]  # sum of loss * n, sum of top-1 % * n, n (this rank)
+    shard_rank = getattr(val_loader, 'rank', 0)
+    shard_world = getattr(val_loader, 'world_size', 1)
+    if shard_world != world:
+        raise ValueError("validate: the loader is sharded over %d ranks but the process group "
+                         "has %d" % (shard_world, world))
+    bs = val_loader.batch_size
+    loss_sum, correct, count = 0.0, 0, 0  # this rank
     tick = time.time()
     with torch.no_grad():
         for i, (images, target) in enumerate(val_loader):
+            gi = shard_rank + i * shard_world  # global batch index
+            if gi > 0 and gi * bs >= eval_samples:
+                break  # the unsharded loop stopped after global batch gi - 1
             if args.gpu is not None:
                 images = images.cuda(args.gpu, non_blocking=True)
                 target = target.cuda(args.gpu, non_blocking=True)
-            seen += len(target) * world
             output = model(images)
             n = images.size(0)
-            loss, acc1 = criterion(output, target).item(), accuracy(output, target, topk=1)
-            totals[0] += loss * n
-            totals[1] += acc1 * n
-            totals[2] += n
+            loss = criterion(output, target).item()
+            hits = correct_count(output, target, topk=1)
+            loss_sum += loss * n
+            correct += hits
+            count += n
             if verbose and i % args.print_freq == 0:  # batch value (running mean)
                 now = time.time()
                 print("Test: [%d/%d]\tTime %.3f\tLoss %.4e (%.4e)\tAcc@1 %.2f (%.2f)" % (
-                    i, len(val_loader), now - tick, loss, totals[0] / totals[2], acc1,
-                    totals[1] / totals[2]))
+                    gi, len(val_loader), now - tick, loss, loss_sum / count, 100.0 * hits / n,
+                    100.0 * correct / count))
                 tick = now
-            if seen >= eval_samples:
-                break
     if world > 1:
         dev = torch.device('cuda', args.gpu) if args.gpu is not None else torch.device('cpu')
-        t = torch.tensor(totals, dtype=torch.float64, device=dev)
+        t = torch.tensor([loss_sum], dtype=torch.float64, device=dev)
+        c = torch.tensor([correct, count], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
-        totals = t.tolist()
-    loss = totals[0] / max(totals[2], 1.0)
-    top1 = totals[1] / max(totals[2], 1.0)
+        dist.all_reduce(c)
+        loss_sum = float(t.item())
+        correct, count = (int(v) for v in c.tolist())
+    loss = loss_sum / max(count, 1)
+    top1 = 100.0 * correct / max(count, 1)
     if verbose:
         print(' * Acc@1 %.3f ' % top1)
     return loss, top1
+
+
+def correct_count(output, target, topk=1):
+    """Rows whose target is among the ``topk`` highest outputs (an exact integer, so
+    per-rank counts all-reduce to exactly the single-process count)."""
+    with torch.no_grad():
+        return int((output.topk(topk, dim=1).indices == target.view(-1, 1)).any(dim=1).sum())
 
 
 def accuracy(output, target, topk=1):

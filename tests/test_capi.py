@@ -189,3 +189,32 @@ def test_swish_epilogue_and_act_encode_act_validation():
                                  8, 1, None) == 1
     assert b"sf" in lib.tq_last_error()
     assert tq_native.act_code("swish") == 3 and tq_native.act_code(6) == 2
+
+
+def test_dwconv_fused_requires_the_epilogue_affine():
+    """tq_dwconv2d_termpair_fused has no scale/bias of its own: an epilogue without
+    ch_scale/ch_shift is rejected (it would otherwise return acc * 0 + 0 everywhere)."""
+    lib = tq_native.lib()
+    buf = torch.zeros(1 << 16, dtype=torch.float32)
+    p = buf.data_ptr()
+    epi = tq_native.DwEpilogue(ch_scale=None, ch_shift=None, relu=1, codes=None, cp=16,
+                               sf=1.0, bits=8, terms=3, fmt=0)
+    rc = lib.tq_dwconv2d_termpair_fused(p, 1, 8, 8, 16, 16, p, 3, 3, 1, 1, 1, 1, 1, 1, p, 8, 8,
+                                        ctypes.byref(epi), None)
+    assert rc == 1 and b"ch_scale" in lib.tq_last_error()
+
+
+def test_fused_conv_code_rows_must_be_roundup_cout():
+    """Epilogue code targets need cp == roundup(cout, 8): the kernels zero the pad channels
+    [cout, cp) only up to the next multiple of 8, so wider rows would keep stale codes."""
+    lib = tq_native.lib()
+    buf = torch.zeros(1 << 16, dtype=torch.float32)
+    p = buf.data_ptr()
+    # (only rejected calls here: an accepted one would launch a kernel on host pointers)
+    for cp_a in (24, 8, 32):
+        epi = tq_native.ConvEpilogue(relu=1, codes_a=p, cp_a=cp_a, sf_a=1.0, bits_a=9,
+                                     terms_a=3, fmt_a=1)
+        rc = lib.tq_conv2d_termpair_fused(p, 1, 8, 8, 16, p, 12, 3, 3, 192, 1, 1, 1, 1, 1, 1,
+                                          1.0, None, p, 8, 8, ctypes.byref(epi), None)
+        err = lib.tq_last_error()
+        assert rc == 1 and b"roundup(cout, 8)" in err, err

@@ -82,3 +82,71 @@ def test_gloo_world2_sharding_histograms_accuracy():
         correct += (net(x).argmax(1) == y).sum().item()
         total += y.numel()
     assert acc0 == pytest.approx(100.0 * correct / total)
+
+
+def _grid_worker(rank, world, port, out_dir, out):
+    """One torchrun-style rank of evaluate_group_size.py on the CPU (--gpu -1: gloo)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "term-quantization_amd"))
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world)})
+    torch.set_num_threads(max(1, 8 // world))
+    import evaluate_cnn
+    import evaluate_group_size
+    seen = []
+    validate = evaluate_cnn.util.validate
+
+    def recording(*a, **k):  # (loss, top1) of every calibration / evaluation pass
+        r = validate(*a, **k)
+        seen.append(r)
+        return r
+    evaluate_cnn.util.validate = recording
+    res = evaluate_group_size.main(["--synthetic", "-a", "resnet18", "--gpu", "-1",
+                                    "--num-samples", "6", "-b", "2", "--image-size", "64",
+                                    "--out-dir", out_dir])
+    out[rank] = (res, seen)
+
+
+def test_evaluate_group_size_world2_equals_world1(tmp_path):
+    """BASELINE configs[4] through the code torchrun launches: evaluate_group_size.py --synthetic
+    on the CPU (gloo) at world 1 and world 2.  Rank-strided batches, histograms summed over
+    ranks and integer counters make the results JSON -- and every (loss, top-1) pass of the
+    25 settings -- identical at both world sizes; the written file equals the returned dict."""
+    import json
+    mgr = mp.Manager()
+    runs = {}
+    for world in (1, 2):
+        out = mgr.dict()
+        d = str(tmp_path / ("w%d" % world))
+        mp.spawn(_grid_worker, args=(world, _free_port(), d, out), nprocs=world, join=True)
+        runs[world] = dict(out)
+        written = json.load(open(os.path.join(d, "resnet18-group-size-results.json")))
+        assert written == runs[world][0][0]
+    r1, seen1 = runs[1][0]
+    r2, seen2 = runs[2][0]
+    assert r1 == r2 and seen1 == seen2 and len(seen1) == 50
+    assert runs[2][1] == runs[2][0]  # both ranks return the global figures
+    pub = json.load(open(os.path.join(HERE, "golden", "published_results.json")))[
+        "resnet18-group-size-results.json"]
+    for g in ("1", "2", "8", "16", "32"):  # the published term-pair MAC counts per setting
+        assert r1[g]["tmacs"] == pub[g]["tmacs"] and r1[g]["avg_terms"] == pub[g]["avg_terms"]
+
+
+def test_sharded_loader_covers_a_map_style_dataset_once():
+    """The ImageFolder path's sharding (util.ShardedLoader / StridedBatchSampler) on a
+    map-style dataset: ranks hold the strided global batches, unpadded, and together they are
+    exactly the unsharded loader's batches -- no duplicated samples in the counters."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "term-quantization_amd"))
+    import util
+    ds = torch.utils.data.TensorDataset(torch.arange(23).float(), torch.arange(23))
+    ds.targets = list(range(23))
+    full = [y.tolist() for _, y in torch.utils.data.DataLoader(ds, batch_size=4)]
+    for world in (1, 2, 3, 8):
+        shards = [util.ShardedLoader(ds, 4, r, world) for r in range(world)]
+        got = {}
+        for r, sh in enumerate(shards):
+            assert len(sh) == len(full) and sh.batch_size == 4 and sh.world_size == world
+            for j, (_, y) in enumerate(sh):
+                got[r + j * world] = y.tolist()
+        assert [got[i] for i in range(len(full))] == full

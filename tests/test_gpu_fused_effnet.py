@@ -160,3 +160,29 @@ def test_fused_efficientnet_b0_matches_module_path(net):
     torch.cuda.synchronize()
     rel = ((a - b).norm() / b.norm()).item()
     assert rel < 5e-2, rel
+
+
+def test_swish_is_torchs_fp32_swish_bit_for_bit():
+    """The fused swish (tq_device.h swish_f32: 1 / (1 + expf(-y)) then y * s, the device
+    library's expf and an IEEE division) equals the module path's MemoryEfficientSwish,
+    x * torch.sigmoid(x) on the GPU, bit for bit -- so codes the fused executor emits after a
+    swish are TR of exactly the value the reference composition computes."""
+    import tq_native
+    torch.manual_seed(3)
+    x = torch.randn(4, 64, 17, 9, device=DEV) * 4
+    flat = x.view(-1)
+    edge = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 88.0, -88.0, 104.0, -104.0, 1e4, -1e4,
+                         float("inf"), float("-inf"), 20.0, -20.0, 0.5, -0.5], device=DEV)
+    flat[:edge.numel()] = edge
+    x = x.contiguous(memory_format=torch.channels_last)
+    out = torch.empty_like(x)
+    codes = torch.empty((4, 17, 9, 64), dtype=torch.float16, device=DEV)
+    tq_native.act_encode_act(x, 0.01, 9, 3, codes, act="swish", out=out)
+    ref = x * torch.sigmoid(x)
+    torch.cuda.synchronize()
+    same = (out.view(torch.int32) == ref.view(torch.int32)) | (torch.isnan(out) & torch.isnan(ref))
+    assert bool(same.all()), int((~same).sum())
+    yq = oracle.tr(out.permute(0, 2, 3, 1).contiguous().cpu().numpy().reshape(1, -1, 1, 1),
+                   0.01, 9, 1, 3)
+    exp = np.rint(yq.reshape(4, 17, 9, 64) / np.float32(0.01)).astype(np.int64)
+    assert np.array_equal(codes.long().cpu().numpy(), exp)

@@ -232,3 +232,95 @@ def fused_next(rec, r):
         if "conv" in q and q["codes_in"] is r["codes_a"]:
             return r["codes_a"], q["conv"].quant
     return None, None
+
+
+def test_calibration_matches_the_reference_fp32_loop(bench_model):
+    """Seam 1, calibration: the literal loop of tr_layer.py:43-54 -- 2048 HIP tr() calls and
+    torch's fp32 (hist * (x - xh)**2).sum() on the GPU, then the first arg-min -- on the 19
+    bench histograms, against the sf tq_mse_profile chose (fp64 sums of the same fp32 per-bin
+    terms).  Where the two differ, the flip must be explained by the reference's own fp32
+    reduction: the exact error gap between the two candidates is no larger than the rounding
+    of the reference's two fp32 sums."""
+    import tr_layer
+    qmodel, _ = bench_model
+    layers = [m for m in qmodel.modules() if isinstance(m, tr_layer.TRConv2dLayer)]
+    assert len(layers) == 19
+    differ = []
+    for li, m in enumerate(layers):
+        q = m.input_quant
+        hist = q.hist_bins
+        x = torch.linspace(q.minv, q.maxv, len(hist)).to(DEV)
+        sfs = torch.linspace(1e-8, q.maxv, 2048).tolist()
+        errs32, errs64 = [], []
+        for sf in sfs:
+            xh = tr_layer.tr_cuda.tr(x.view(-1, 1, 1, 1), sf, q.data_bits, 1,
+                                     q.data_terms).view(-1)
+            t = hist * (x - xh) ** 2
+            errs32.append(t.sum())
+            errs64.append(t.double().sum())
+        e32 = torch.stack(errs32).cpu()
+        e64 = torch.stack(errs64).cpu()
+        i_ref = int(torch.argmin(e32).item())
+        sf_ref = sfs[i_ref]
+        i_got = sfs.index(q.sf)
+        if i_got != i_ref:
+            gap = float(e64[i_ref] - e64[i_got])
+            rnd = abs(float(e32[i_ref]) - float(e64[i_ref])) + \
+                abs(float(e32[i_got]) - float(e64[i_got]))
+            assert 0.0 <= gap <= rnd, (li, i_ref, i_got, gap, rnd)
+            differ.append((li, i_ref, i_got, gap, rnd))
+        else:
+            assert q.sf == sf_ref
+    print("calibration seam: %d of 19 bench layers pick a different sf than the reference's "
+          "fp32 loop %s" % (len(differ), differ))
+
+
+def test_fused_stem_codes_vs_miopen_fp32_stem(bench_model):
+    """Seam 2, the stem: layer1.0's input codes from the fused stem (split-fp16 near-fp32 conv,
+    DESIGN 4.3) against oracle.tr() of the module path's stem -- MIOpen's fp32 conv1 -> bn1 ->
+    relu -> maxpool, the reference composition -- on the whole 256-image bench batch.  Every
+    differing code must be a one-step straddle of a rounding midpoint (the quantized integers
+    differ by one and the midpoint lies between the two fp32 quotients), and the flips must be
+    at most 1e-4 of the codes."""
+    from concurrent.futures import ThreadPoolExecutor
+    qmodel, x = bench_model
+    fused = tq_fuse.FusedResNet(qmodel)
+    assert fused.stem_w is not None
+    with torch.no_grad():
+        rec = []
+        fused(x, capture=rec)
+        m = qmodel
+        ref = m.maxpool(m.relu(m.bn1(m.conv1(x)))).contiguous(memory_format=torch.channels_last)
+    stem = rec[0]
+    conv = rec[1]["conv"]
+    codes = rec[1]["codes_in"]          # layer1.0.conv1's input codes = the stem's codes
+    sf, db, dt = conv.quant
+    c = 64
+    got = codes[..., :c].float().cpu().numpy().astype(np.int64)      # [N, H, W, C]
+    yref = ref.permute(0, 2, 3, 1).contiguous().cpu().numpy()         # NHWC fp32
+    yfus = stem["out"].permute(0, 2, 3, 1).contiguous().cpu().numpy()
+    flat = yref.reshape(-1)
+    out = np.empty_like(flat)
+    bounds = np.linspace(0, flat.size, 33).astype(np.int64)
+
+    def run(j):
+        lo, hi = bounds[j], bounds[j + 1]
+        out[lo:hi] = oracle.tr(flat[lo:hi].reshape(1, -1, 1, 1), sf, db, 1, dt).reshape(-1)
+    with ThreadPoolExecutor(8) as ex:
+        list(ex.map(run, range(32)))
+    exp = np.rint(out.astype(np.float64) / float(np.float32(sf))).astype(np.int64).reshape(
+        got.shape)
+    mism = got != exp
+    flips, total = int(mism.sum()), got.size
+    if flips:
+        qm, qf = _quantize(yref[mism], conv.quant), _quantize(yfus[mism], conv.quant)
+        assert np.all(np.abs(qm - qf) == 1)
+        mid = np.minimum(qm, qf).astype(np.float64) + 0.5
+        s32 = np.float32(sf)
+        rm = (np.abs(yref[mism]) / s32).astype(np.float32).astype(np.float64)
+        rf = (np.abs(yfus[mism]) / s32).astype(np.float32).astype(np.float64)
+        lo, hi = np.minimum(rm, rf), np.maximum(rm, rf)
+        assert np.all((lo <= mid) & (mid <= hi))
+    print("stem seam: %d of %d layer1.0 input codes differ from TR of the MIOpen fp32 stem "
+          "(%.2e)" % (flips, total, flips / total))
+    assert flips <= total * 1e-4, (flips, total)

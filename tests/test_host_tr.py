@@ -255,3 +255,30 @@ def test_evaluate_mlp_runs_on_cpu(tmp_path):
     assert res["tmacs"][1] == pub["tmacs"][3]
     # g=8, k=12 has no published point; same formula, alpha = k/g twice the g=16 one
     assert res["tmacs"][0] == 2 * pub["tmacs"][3]
+
+
+@pytest.mark.gpu
+def test_evaluate_mlp_runs_on_cpu_in_gpu_run(tmp_path):
+    """The same BASELINE configs[0] run (CPU torch, host TR op) inside the -m gpu selection,
+    so the round-end GPU-box run records the MNIST MLP config too."""
+    test_evaluate_mlp_runs_on_cpu(tmp_path)
+
+
+def test_lstm_termpair_falls_back_past_the_int32_bound():
+    """TRLSTMLayer keeps its term-pair path only while the exact int32 sums cannot wrap
+    (sum_k |v_w| << data_bits < 2^31 for both layer-0 weights, as TRConv2dLayer and
+    TRLinearLayer check it); at 14-bit weights and activations over K = 650 they can, so the
+    layer falls back to the reference composition (library LSTM on TR'd tensors)."""
+    torch.manual_seed(0)
+    ok = tr_layer.TRLSTMLayer(nn.LSTM(650, 650, 2), 8, 8, 8, 8, 12)
+    assert ok.termpair and hasattr(ok, "w_codes_ih") and hasattr(ok, "w_codes_hh")
+    lstm = nn.LSTM(650, 650, 2)
+    w_hh = lstm.weight_hh_l0.detach().clone()
+    big = tr_layer.TRLSTMLayer(lstm, 14, 8, 14, 8, 12)
+    assert not big.termpair
+    assert not hasattr(big, "w_codes_ih") and not hasattr(big, "w_codes_hh")
+    # weights still TR'd (bit-exact vs the oracle); w_sf is the hh scale, as the reference's
+    sf = w_hh.abs().max().item() / 2**13
+    assert big.w_sf == sf
+    assert torch.equal(big.lstm.weight_hh_l0.detach(),
+                       torch.from_numpy(oracle.tr(w_hh.numpy(), sf, 14, 8, 12)))

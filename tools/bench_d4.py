@@ -62,6 +62,10 @@ def kernel_breakdown(fn, steps, total_s):
             tf = 2 * k["work"] / k["seconds"] / 1e12
             e.update({"bound": "mfma", "achieved_tflops": tf, "peak_tflops": MFMA_F16_PEAK_TFLOPS,
                       "frac": tf / MFMA_F16_PEAK_TFLOPS})
+            if k["bytes"]:  # fused convs state their algorithmic bytes: the HBM side too
+                gbs = k["bytes"] / k["seconds"] / 1e9
+                e.update({"achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
+                          "hbm_frac": gbs / HBM_PEAK_GBS})
         elif name in ("act_encode", "act_encode_act"):
             gbs = k["work"] / k["seconds"] / 1e9
             e.update({"bound": "hbm", "achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
@@ -193,6 +197,51 @@ def cnn(arch, args, dev):
                                    % arch, "batch": args.batch, "layer_modes": modes,
                        "data": "synthetic N(0,1), random-init weights"},
             "kernels": kernels, "fused_executor": fused}
+
+
+def cnn_fused(arch, steps, warmup, batch, dev):
+    """The fused executor of a depthwise config alone (bench.py's d4 key): images/s and the
+    per-kernel rooflines.  Every term-pair conv of these executors is a 1x1 conv with
+    Cin <= 960 whose bytes outweigh its products (codes in, fp32/codes out), so it is priced
+    against HBM, as the depthwise and encode kernels are."""
+    torch.manual_seed(0)
+    model = getattr(cnn_models, arch)(pretrained=False).to(dev).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(batch, 3, 224, 224, device=dev).contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        q(x)
+        tr_layer.set_tr_tracking(q, False)
+        ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
+              tq_fuse.FusedEfficientNet)(q)
+        tf = timed(lambda: ex(x), steps, warmup)
+        kern = kernel_breakdown(lambda: ex(x), steps, tf)
+    tp = kern.get("conv2d_termpair")
+    if tp is not None:  # 1x1 convs: HBM-bound (algorithmic bytes per launch, fused _Conv)
+        tp.update({"bound": "hbm", "mfma_frac": tp.pop("frac"), "frac": tp.pop("hbm_frac", None)})
+    dom = max(kern, key=lambda k: kern[k]["share_of_step"])
+    return {"images_per_s": batch / tf, "ms_per_step": tf * 1e3, "batch": batch,
+            "dominant_kernel": dom, "kernels": kern}
+
+
+def d4_summary(dev, steps=5, warmup=2, batch=256):
+    """BASELINE configs[2] and [3] on one GPU, compactly (bench.py's "d4" key): LSTM-650
+    tokens/s (term-pair layer-0 path and the MIOpen composition) with the term-pair decoder
+    GEMM's roofline; fused MobileNet-V2 / EfficientNet-b0 images/s with per-kernel rooflines."""
+    a = argparse.Namespace(steps=steps, warmup=warmup, batch=batch)
+    out = {}
+    r = lstm(a, dev)
+    out["lstm650"] = {"tokens_per_s": r["termpair_lstm_tokens_per_s"],
+                      "tokens_per_s_miopen_composition": r["value"],
+                      "dominant_kernel": "term-pair decoder GEMM (650 -> 33278, 350 rows)",
+                      "roofline": dict(r["term_pair_decoder"], bound="mfma",
+                                       peak_tflops=MFMA_F16_PEAK_TFLOPS,
+                                       frac=r["term_pair_decoder"]["frac_of_fp16_mfma_peak"]),
+                      "config": r["config"]}
+    for arch in ("mobilenet_v2", "efficientnet_b0"):
+        out[arch] = cnn_fused(arch, steps, warmup, batch, dev)
+    return out
 
 
 def main():
