@@ -24,14 +24,16 @@ __device__ int4 g_dw_zero;  // zero-initialised static storage, never written: p
 // Operands known to fit 24 signed bits let the compiler emit v_mad_i32_i24 (full rate).
 __device__ __forceinline__ int sext24(int v) { return (v << 8) >> 8; }
 
-// Epilogue of output pixel p (image img, in-image index rem), channels c0 .. c0 + 7, from the
-// exact int32 sums: one fp64 -> fp32 rounding, activation, fp32 store and/or next codes.
-__device__ __forceinline__ void dw_emit8(const DwConvArgs& a, const uint16_t* lut, int64_t p,
-                                         int64_t img, int rem, int c0, const int acc[8]) {
+// Epilogue of output pixel p (image img, in-image index rem), channels c0 .. c0 + CPL - 1,
+// from the exact int32 sums: one fp64 -> fp32 rounding, activation, fp32 store and/or next
+// codes.  CPL = 4 or 8 channels per lane.
+template <int CPL>
+__device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut, int64_t p,
+                                        int64_t img, int rem, int c0, const int acc[CPL]) {
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
-  float y[8];
+  float y[CPL];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < CPL; ++i) {
     const int c = c0 + i;
     if (a.ch_scale) {  // folded BN (pad channels: 0)
       y[i] = c < a.C ? (float)((double)acc[i] * a.ch_scale[c] + a.ch_shift[c]) : 0.0f;
@@ -40,54 +42,59 @@ __device__ __forceinline__ void dw_emit8(const DwConvArgs& a, const uint16_t* lu
       y[i] = (float)((double)acc[i] * a.scale + sh);
     }
   }
-  if (a.relu) {  // ReLU / ReLU6 / swish; the stored value keeps a NaN (torch.relu / hardtanh)
-    float o[8];
+  const bool full = (a.C % CPL) == 0;
+  auto store_nhwc = [&](const float (&v)[CPL]) {
+    float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
+    if (full) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) act_apply(a.relu, y[i], o[i]);
-    if (a.out) {
-      float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
-      if ((a.C & 7) == 0) {
-        *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (c0 + i < a.C) dst[i] = o[i];
-      }
-    }
-  }
-  if (a.codes) {  // next layer's codes of channels c0 .. c0 + 7 (cp_c == Cp: same channels)
-    uint32_t v[8];
-    if (a.lut_c) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = lut[relu_q(y[i], a.inv_c, a.maxv_c)];
+      for (int i = 0; i < CPL; i += 4)
+        *reinterpret_cast<float4*>(dst + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = code_bits(tr_value_g1_inv(y[i], a.inv_c, a.maxv_c, a.k_c), a.fmt_c);
+      for (int i = 0; i < CPL; ++i)
+        if (c0 + i < a.C) dst[i] = v[i];
+    }
+  };
+  if (a.relu) {  // ReLU / ReLU6 / swish; the stored value keeps a NaN (torch.relu / hardtanh)
+    float o[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) act_apply(a.relu, y[i], o[i]);
+    if (a.out) store_nhwc(o);
+  }
+  if (a.codes) {  // next layer's codes of channels c0 .. c0 + CPL - 1 (cp_c == Cp)
+    uint32_t v[CPL];
+    if (a.lut_c) {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) v[i] = lut[relu_q(y[i], a.inv_c, a.maxv_c)];
+    } else {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        v[i] = code_bits(tr_value_g1_inv(y[i], a.inv_c, a.maxv_c, a.k_c), a.fmt_c);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < CPL; ++i)
       if (c0 + i >= a.C) v[i] = 0u;  // pad channels: zero codes
-    *reinterpret_cast<uint4*>(a.codes + p * a.cp_c + c0) =
-        make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
-                   v[6] | (v[7] << 16));
+    if (CPL == 8)
+      *reinterpret_cast<uint4*>(a.codes + p * a.cp_c + c0) =
+          make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4 % CPL] | (v[5 % CPL] << 16),
+                     v[6 % CPL] | (v[7 % CPL] << 16));
+    else
+      *reinterpret_cast<uint2*>(a.codes + p * a.cp_c + c0) =
+          make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
   }
   if (a.relu || !a.out) return;
   if (a.out_nhwc) {
-    float* dst = a.out + p * a.C + c0;
-    if ((a.C & 7) == 0) {
-      *reinterpret_cast<float4*>(dst) = make_float4(y[0], y[1], y[2], y[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(y[4], y[5], y[6], y[7]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (c0 + i < a.C) dst[i] = y[i];
-    }
+    store_nhwc(y);
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < CPL; ++i)
       if (c0 + i < a.C) a.out[(img * a.C + c0 + i) * HoWo + rem] = y[i];
   }
+}
+
+__device__ __forceinline__ void dw_emit8(const DwConvArgs& a, const uint16_t* lut, int64_t p,
+                                         int64_t img, int rem, int c0, const int acc[8]) {
+  dw_emit<8>(a, lut, p, img, rem, c0, acc);
 }
 
 __global__ __launch_bounds__(256) void dwconv_tp_kernel(DwConvArgs a) {
@@ -208,13 +215,131 @@ __global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
   }
 }
 
+// Sliding-window 3x3 depthwise kernel (dilation 1, stride S = 1 or 2): a lane owns CPL
+// channels of one output column over R consecutive output rows.  The nine taps' weights stay
+// in registers for all R rows; the input rows are a window of three tap rows (each the three
+// column taps, CPL codes apiece) that slides down by S rows per output row, and the S rows
+// the next output row adds are loaded while the current one computes and runs its epilogue:
+// every input row is loaded once per lane (S + (3 - S) / R rows per output instead of 3 per
+// output and 9 loads), and the loads stream with no round trip of their own.  Taps in the
+// padding read a zero block (unconditional loads).  Lanes run chunk-fastest, then along the
+// output row, so a wave's load of one tap covers contiguous NHWC bytes.
+template <int S, int R, int CPL>
+__global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
+  if (a.lut_c) {
+    lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
+    __syncthreads();
+  }
+  typedef int v4i __attribute__((ext_vector_type(CPL / 2)));  // CPL int16 codes
+  const int chunks = a.Cp / CPL;
+  const int nrb = (a.Ho + R - 1) / R;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t lanes = (int64_t)a.N * nrb * a.Wo * chunks;
+  if (t >= lanes) return;
+  int64_t q = t / chunks;
+  const int c0 = (int)(t - q * chunks) * CPL;
+  const int ow = (int)(q % a.Wo);
+  q /= a.Wo;
+  const int rb = (int)(q % nrb);
+  const int64_t img = q / nrb;
+  const int oh0 = rb * R;
+  const int iw0 = ow * S - a.pw;
+  int w[9][CPL];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int32_t* wt = a.w + (int64_t)k * a.Cp + c0;
+#pragma unroll
+    for (int i = 0; i < CPL; i += 4) {
+      const int4 wv = *reinterpret_cast<const int4*>(wt + i);
+      w[k][i] = sext24(wv.x);
+      w[k][i + 1] = sext24(wv.y);
+      w[k][i + 2] = sext24(wv.z);
+      w[k][i + 3] = sext24(wv.w);
+    }
+  }
+  bool cok[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) cok[ks] = iw0 + ks >= 0 && iw0 + ks < a.W;
+  const int16_t* xb = a.x + (int64_t)img * a.H * a.W * a.Cp + c0;
+  const v4i* zero = reinterpret_cast<const v4i*>(&g_dw_zero);
+  auto load_row = [&](int ih, v4i (&dst)[3]) {
+    const bool rok = ih >= 0 && ih < a.H;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const bool ok = rok && cok[ks];
+      dst[ks] = *(ok ? reinterpret_cast<const v4i*>(xb + ((int64_t)ih * a.W + iw0 + ks) * a.Cp)
+                     : zero);
+    }
+  };
+  const uint16_t* l = a.lut_c ? lut : nullptr;
+  const int ih0 = oh0 * S - a.ph;  // first tap row of output row oh0
+  v4i win[3][3];
+#pragma unroll
+  for (int kr = 0; kr < 3; ++kr) load_row(ih0 + kr, win[kr]);
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    // the S new tap rows of output row j + 1, in flight during row j's MACs and epilogue
+    v4i nxt[S][3];
+    if (j + 1 < R) {
+#pragma unroll
+      for (int u = 0; u < S; ++u) load_row(ih0 + (j + 1) * S + 3 - S + u, nxt[u]);
+    }
+    int acc[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) acc[i] = 0;
+#pragma unroll
+    for (int kr = 0; kr < 3; ++kr)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const v4i xv = win[kr][ks];
+#pragma unroll
+        for (int i = 0; i < CPL / 2; ++i) {
+          const int lo = (int)(short)(xv[i] & 0xFFFF);
+          const int hi = xv[i] >> 16;
+          acc[2 * i] += lo * w[kr * 3 + ks][2 * i];
+          acc[2 * i + 1] += hi * w[kr * 3 + ks][2 * i + 1];
+        }
+      }
+    const int oh = oh0 + j;
+    if (oh < a.Ho)
+      dw_emit<CPL>(a, l, (img * a.Ho + oh) * a.Wo + ow, img, oh * a.Wo + ow, c0, acc);
+    if (j + 1 < R) {
+#pragma unroll
+      for (int kr = 0; kr < 3; ++kr)
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks)
+          win[kr][ks] = kr + S < 3 ? win[kr + S][ks] : nxt[kr + S - 3][ks];
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.N * a.Ho * a.Wo * (a.Cp / 8);
   if (n == 0) return hipSuccess;
-  // A/B override (tools only): TQ_DW_ROWS=0 the flat kernel, =4 four rows for 5x5 too
+  // A/B override (tools only): TQ_DW_ROWS=0 the flat kernel, =4 four rows for 5x5 too;
+  // TQ_DW_SLIDE=0 keeps 3x3 convs on the row-blocked kernel, =4 four channels per lane
   static const char* rows_env = getenv("TQ_DW_ROWS");
+  const char* slide_env = getenv("TQ_DW_SLIDE");  // read per launch: tests switch it
+  const int slide = slide_env ? atoi(slide_env) : 4;
+  if (slide && !(rows_env && atoi(rows_env) == 0) && a.KH == 3 && a.KW == 3 && a.dh == 1 &&
+      a.dw == 1 && a.sh == a.sw && (a.sh == 1 || a.sh == 2) && a.Cp % slide == 0) {
+    constexpr int R = 8;
+    const int cpl = slide == 4 ? 4 : 8;
+    const int64_t lanes = (int64_t)a.N * ((a.Ho + R - 1) / R) * a.Wo * (a.Cp / cpl);
+    const dim3 grid((unsigned)((lanes + 255) / 256));
+    const size_t lds = (size_t)a.lut_c * 2;
+    if (cpl == 8) {
+      if (a.sh == 1) dwconv3_slide_kernel<1, R, 8><<<grid, 256, lds, stream>>>(a);
+      else dwconv3_slide_kernel<2, R, 8><<<grid, 256, lds, stream>>>(a);
+    } else {
+      if (a.sh == 1) dwconv3_slide_kernel<1, R, 4><<<grid, 256, lds, stream>>>(a);
+      else dwconv3_slide_kernel<2, R, 4><<<grid, 256, lds, stream>>>(a);
+    }
+    return hipGetLastError();
+  }
   if (!(rows_env && atoi(rows_env) == 0) && a.dh == 1 && a.dw == 1 &&
       ((a.KH == 3 && a.KW == 3) || (a.KH == 5 && a.KW == 5))) {
     // four output rows per lane for 3x3, two for 5x5 (four would need 180 VGPRs)

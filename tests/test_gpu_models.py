@@ -178,3 +178,44 @@ def test_depthwise_models_layers_match_reference_composition(arch):
     assert "reference" not in modes  # every converted layer runs a term-pair kernel
     if arch == "efficientnet_b0":
         assert "wide" in modes  # the (16, 1, 16) squeeze-excite convs
+
+
+@pytest.mark.parametrize("cfg", [
+    # c, hw, stride, pad (top, left), ho/wo: plain 3x3 s1 p1, s2 p1 (odd input), MobileNet-V2
+    # shapes, static-same s2 (pad 0 top/left, EfficientNet), H % 8 != 0, Cp with pad channels
+    (32, 14, 1, (1, 1)), (96, 15, 2, (1, 1)), (144, 28, 2, (1, 1)), (40, 13, 1, (1, 1)),
+    (24, 16, 2, (0, 0)), (20, 9, 1, (1, 1)), (960, 7, 1, (1, 1)),
+])
+@pytest.mark.parametrize("relu", [6, "swish"])
+def test_dw_sliding_window_kernel_bit_identical(cfg, relu, monkeypatch):
+    """The sliding-window 3x3 depthwise kernel (tr_dwconv.hip dwconv3_slide_kernel, 4 or 8
+    channels per lane, weights in registers, tap rows streamed once) against the row-blocked
+    kernel (TQ_DW_SLIDE=0): the same exact int32 sums and epilogue, so the fp32 outputs and the
+    next layer's codes are bit-identical, including partial row blocks, odd sizes, stride 2 and
+    asymmetric (static-same) padding."""
+    import tq_native
+    c, hw, s, (pt, pl) = cfg
+    torch.manual_seed(c + hw)
+    conv = nn.Conv2d(c, c, 3, s, 1, groups=c, bias=False)
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 16, 1, 16)
+    cp = layer.act_channels
+    x = torch.relu(torch.randn(3, c, hw, hw, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.zeros((3, hw, hw, cp), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    ho = (hw + pt + (1 if s == 2 and pt == 0 else 1) - 3) // s + 1
+    sc = torch.rand(c, dtype=torch.float64, device=DEV) * 1e-5
+    sh = torch.randn(c, dtype=torch.float64, device=DEV) * 0.1
+    outs = []
+    for mode in ("0", "4", "8"):
+        monkeypatch.setenv("TQ_DW_SLIDE", mode)
+        o = torch.full((3, c, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        nc = torch.full((3, ho, ho, cp), -1, dtype=torch.int16, device=DEV)
+        tq_native.dwconv2d_termpair_fused(codes, c, layer.w_codes, 3, 3, (s, s), (pt, pl),
+                                          (1, 1), ho, ho, sc, sh, relu, out=o, next_codes=nc,
+                                          quant=(0.03, 9, 3))
+        outs.append((o.view(torch.int32).cpu(), nc.cpu()))
+    for o, nc in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(nc, outs[0][1])
+    assert not torch.isnan(outs[0][0].view(torch.float32)).any()
