@@ -42,12 +42,13 @@ const char *tq_version(void);
 const char *tq_last_error(void);
 
 /*
- * Diagnostics: the number of bounded team-sync waits of the row-strip conv engine that ran
- * out since the previous call (each one means a launch went on without confirming that its
- * LDS patch was staged, so its results are suspect), then clears the count.  Synchronous
- * (waits for the device); `count` is a host pointer.  A healthy run reads 0.
+ * Diagnostics: the number of bounded in-kernel waits that ran out since the previous call --
+ * the row-strip conv engine's team syncs and tq_lstm_seq_f32's step exchange (each one means
+ * a launch went on without confirming data it waited for, so its results are suspect) --
+ * then clears the count.  Synchronous (waits for the device); `count` is a host pointer.  A
+ * healthy run reads 0.
  */
-int tq_strip_sync_faults(uint32_t *count);
+int tq_sync_faults(uint32_t *count);
 
 /*
  * Term-revealing op, float32 / float64.  Replaces the pybind entry
@@ -373,6 +374,23 @@ int tq_mse_profile(const float *x, const float *hist, int64_t nbins, const float
  */
 int tq_lstm_cell_f32(const float *gx, const float *hh, float *c, float *h, int64_t batch,
                      int64_t hidden, void *stream);
+
+/*
+ * A whole LSTM layer's recurrence (torch.nn.LSTM semantics, gate order i, f, g, o) in one
+ * persistent launch, replacing T x (a recurrent-projection GEMM + tq_lstm_cell_f32) of
+ * TRLSTMLayer's per-step loop (tr_layer.py:191-195 runs cuDNN's LSTM there):
+ *   gates_t = gx[t] + b_hh + h_{t-1} W_hh^T,  c_t = sigmoid(f) c_{t-1} + sigmoid(i) tanh(g),
+ *   h_t = sigmoid(o) tanh(c_t),  out[t] = h_t,  for t < steps, from (h0, c0)
+ * gx [steps][batch][4 hidden] (the input projection incl. b_ih), w_hh [4 hidden][hidden],
+ * b_hh [4 hidden] (or NULL), h0/c0/c_out [batch][hidden], out [steps][batch][hidden], all fp32
+ * device buffers; c_out = c_{steps-1} (h_{steps-1} is out[steps-1]).  `workspace` >=
+ * tq_lstm_seq_workspace_bytes(batch, hidden) device bytes, zeroed by the call (enqueued).
+ * Domain: hidden <= 1024, batch * hidden <= 16384.  fp32 arithmetic, a fixed summation order.
+ */
+int64_t tq_lstm_seq_workspace_bytes(int64_t batch, int64_t hidden);
+int tq_lstm_seq_f32(const float *gx, const float *w_hh, const float *b_hh, const float *h0,
+                    const float *c0, float *out, float *c_out, int64_t steps, int64_t batch,
+                    int64_t hidden, void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * Tracking histogram of the activation calibration, replacing

@@ -78,9 +78,14 @@ const char* tq_version(void) { return "tq-hip 0.1.0 gfx950"; }
 
 const char* tq_last_error(void) { return g_err; }
 
-int tq_strip_sync_faults(uint32_t* count) {
-  if (count == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "strip_sync_faults: count is null");
-  return hip_status(tq::strip_sync_faults(count), "strip_sync_faults");
+int tq_sync_faults(uint32_t* count) {
+  if (count == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "sync_faults: count is null");
+  uint32_t strip = 0, seq = 0;
+  int rc = hip_status(tq::strip_sync_faults(&strip), "sync_faults");
+  if (rc != TQ_OK) return rc;
+  rc = hip_status(tq::lstm_seq_faults(&seq), "sync_faults");
+  *count = strip + seq;
+  return rc;
 }
 
 int tq_tr_f32(const float* input, float* output, int64_t ndim, const int64_t* shape, float sf,
@@ -688,6 +693,27 @@ int tq_lstm_cell_f32(const float* gx, const float* hh, float* c, float* h, int64
     return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_cell: null pointer");
   return hip_status(tq::launch_lstm_cell(gx, hh, c, h, batch, hidden, (hipStream_t)stream),
                     "lstm_cell launch");
+}
+
+int64_t tq_lstm_seq_workspace_bytes(int64_t batch, int64_t hidden) {
+  return tq::lstm_seq_workspace_bytes(batch, hidden);
+}
+
+int tq_lstm_seq_f32(const float* gx, const float* w_hh, const float* b_hh, const float* h0,
+                    const float* c0, float* out, float* c_out, int64_t steps, int64_t batch,
+                    int64_t hidden, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (steps < 0 || batch < 0 || hidden < 0 || hidden > 1024 || batch * hidden > 16384)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: sizes outside hidden <= 1024, batch * "
+                "hidden <= 16384");
+  if (steps * batch * hidden == 0) return TQ_OK;
+  if (!gx || !w_hh || !h0 || !c0 || !out || !c_out || !workspace)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: null pointer");
+  if (workspace_bytes < tq::lstm_seq_workspace_bytes(batch, hidden) ||
+      (uintptr_t)workspace % 16)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: workspace too small or misaligned");
+  return hip_status(tq::launch_lstm_seq(gx, w_hh, b_hh, h0, c0, out, c_out, steps, batch,
+                                        hidden, workspace, (hipStream_t)stream),
+                    "lstm_seq launch");
 }
 
 int tq_histc_f32(const float* x, int64_t numel, int64_t nbins, float minv, float maxv,

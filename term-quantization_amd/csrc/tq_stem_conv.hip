@@ -72,7 +72,7 @@ __device__ __forceinline__ float row_down(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(b, b, 0x100 + D, 0xf, 0xf, false));
 }
 
-template <int TP>
+template <int TP, int QMAX>
 __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArgs a, int sc,
                                                                          int nb, int tiles) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds_raw[];
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   // (3W floats).  The s2d halo columns (input columns outside the image) stay zero.
   constexpr int ROWS = 2 * (2 * TP + 4);
   constexpr int RPW = (ROWS + 7) / 8;
-  constexpr int QMAX = 4;  // float4 per lane and row: W <= 340
+  // QMAX float4 per lane and input row: W <= 64 * QMAX * 4 / 3 (3: W <= 256, 4: W <= 340)
   const int f4n = 3 * a.W / 4;
   for (int i = tid; i < (2 * TP + 4) * sc * 3; i += kStemThreads)
     reinterpret_cast<float4*>(xs)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   }
 }
 
-template <int TP>
+template <int TP, int QMAX>
 hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   const int nb = (a.Wo + 6) / 7;
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
@@ -401,7 +401,7 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   }
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP, QMAX>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kStemDynLds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -413,8 +413,8 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
     cus = 256;
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return hipSuccess;
-  stem_conv_pool_kernel<TP><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(b, sc, nb,
-                                                                                 tiles);
+  stem_conv_pool_kernel<TP, QMAX><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(
+      b, sc, nb, tiles);
   return hipGetLastError();
 }
 
@@ -426,11 +426,12 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
 // rows), else two (measured 717 vs 793 us for the ResNet-18 bench batch).
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream) {
   static const char* tp = getenv("TQ_STEM_TP");  // A/B override (tools only)
+  const bool narrow = 3 * a.W <= 64 * 3 * 4;  // every input row in 3 float4 per lane
   if (!(tp && atoi(tp) == 2)) {
-    const hipError_t e = launch_stem_tp<4>(a, stream);
+    const hipError_t e = narrow ? launch_stem_tp<4, 3>(a, stream) : launch_stem_tp<4, 4>(a, stream);
     if (e != hipErrorInvalidConfiguration) return e;
   }
-  return launch_stem_tp<2>(a, stream);
+  return narrow ? launch_stem_tp<2, 3>(a, stream) : launch_stem_tp<2, 4>(a, stream);
 }
 
 }  // namespace tq

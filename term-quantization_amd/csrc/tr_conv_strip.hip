@@ -60,7 +60,7 @@ __host__ __device__ inline int64_t strip_lds_bytes(int64_t w) {
   return ((int64_t)kStripWUnits + 2 * strip_patch_px((int)w) * 8 + 64) * 16 + 16;
 }
 
-// Team-sync guard exhaustions since the last tq_strip_sync_faults() (device-wide; a
+// Team-sync guard exhaustions since the last tq_sync_faults() (device-wide; a
 // non-zero count means some launch computed with a patch whose staging was not confirmed).
 __device__ uint32_t g_strip_sync_faults;
 
@@ -81,7 +81,7 @@ __device__ __forceinline__ void team_sync(uint32_t* ctr, uint32_t target) {
     __builtin_amdgcn_s_sleep(1);
   }
   // guard exhausted: the protocol broke and this wave goes on with a patch that may be
-  // partly staged -- count it where the host can see it (tq_strip_sync_faults)
+  // partly staged -- count it where the host can see it (tq_sync_faults)
   if (guard == (1 << 22) && (threadIdx.x & 63) == 0)
     __hip_atomic_fetch_add(&g_strip_sync_faults, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

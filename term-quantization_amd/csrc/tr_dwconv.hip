@@ -45,7 +45,8 @@ __device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut
   const bool full = (a.C % CPL) == 0;
   auto store_nhwc = [&](const float (&v)[CPL]) {
     float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
-    if (full) {
+    if (full) {  // a whole chunk inside [0, C), or a pad chunk (nothing to store)
+      if (c0 >= a.C) return;
 #pragma unroll
       for (int i = 0; i < CPL; i += 4)
         *reinterpret_cast<float4*>(dst + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);

@@ -35,7 +35,9 @@ _vp = ctypes.c_void_p
 _SIGNATURES = {
     "tq_version": [],
     "tq_last_error": [],
-    "tq_strip_sync_faults": [ctypes.POINTER(ctypes.c_uint32)],
+    "tq_sync_faults": [ctypes.POINTER(ctypes.c_uint32)],
+    "tq_lstm_seq_workspace_bytes": [_i64, _i64],
+    "tq_lstm_seq_f32": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp],
     "tq_tr_f32": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
@@ -115,7 +117,7 @@ def code_format(codes):
 _RESTYPE = {"tq_version": ctypes.c_char_p, "tq_last_error": ctypes.c_char_p,
             "tq_conv2d_cout_align": _i64, "tq_conv2d_num_configs": _i32,
             "tq_conv2d_mfma_num_configs": _i32,
-            "tq_conv2d_workspace_bytes": _i64}
+            "tq_conv2d_workspace_bytes": _i64, "tq_lstm_seq_workspace_bytes": _i64}
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 
@@ -221,12 +223,35 @@ def version():
     return lib().tq_version().decode()
 
 
-def strip_sync_faults():
-    """Row-strip engine team-sync waits that ran out since the last call (then cleared;
-    synchronous): 0 in a healthy run (tq_strip_sync_faults)."""
+def sync_faults():
+    """Bounded in-kernel waits (row-strip team syncs, LSTM step exchange) that ran out since
+    the last call (then cleared; synchronous): 0 in a healthy run (tq_sync_faults)."""
     n = ctypes.c_uint32(0)
-    _check(lib().tq_strip_sync_faults(ctypes.byref(n)))
+    _check(lib().tq_sync_faults(ctypes.byref(n)))
     return int(n.value)
+
+
+_lstm_ws = {}
+
+
+def lstm_seq(gx, w_hh, b_hh, h0, c0, out, c_out):
+    """A whole LSTM layer's recurrence in one persistent launch (tq_lstm_seq_f32): gx
+    [T, B, 4H], w_hh [4H, H], b_hh [4H] or None, h0/c0/c_out [B, H], out [T, B, H], contiguous
+    fp32 CUDA tensors; the workspace is cached per (device, B, H)."""
+    t, b, h4 = gx.shape
+    hid = h4 // 4
+    key = (gx.device, b, hid)
+    ws = _lstm_ws.get(key)
+    if ws is None:
+        nb = int(lib().tq_lstm_seq_workspace_bytes(b, hid))
+        ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=gx.device)
+        _lstm_ws[key] = ws
+    with torch.cuda.device(gx.device):
+        rc = lib().tq_lstm_seq_f32(_ptr(gx), _ptr(w_hh), _ptr(b_hh), _ptr(h0), _ptr(c0),
+                                   _ptr(out), _ptr(c_out), t, b, hid, _ptr(ws), ws.numel(),
+                                   _stream(gx))
+    _check(rc)
+    return out
 
 
 def _check(rc):

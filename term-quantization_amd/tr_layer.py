@@ -8,6 +8,7 @@ Same public names, constructor signatures, attributes and behaviour as the refer
 tensors: it accumulates term pairs exactly in the term-pair kernel (tq_ops.tr_conv2d).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -451,24 +452,54 @@ class TRLSTMLayer(nn.Module):
         T, B, _ = emb.shape
         H = l.hidden_size
         gx = self._tp_linear(emb.contiguous(), 'ih', l.bias_ih_l0).contiguous()  # [T, B, 4H]
-        w_hh = l.weight_hh_l0
-        c = cq[0].contiguous().clone()
         out0 = torch.empty((T, B, H), dtype=emb.dtype, device=emb.device)
-        h = None
-        for t in range(T):
-            if t == 0:  # TR(h0) x TR(W_hh): term-pair
-                hh = self._tp_linear(h0[0].contiguous(), 'hh', l.bias_hh_l0)
-            else:
-                hh = torch.addmm(l.bias_hh_l0, h, w_hh.t())
-            tq_native.lstm_cell(gx[t], hh.contiguous(), c, out0[t])
-            h = out0[t]
-        hn, cn = [out0[T - 1]], [c]
-        out = out0
-        if self._upper is not None:
+        if not self._seq_kernel(B, H):  # per-step launches (TQ_LSTM_SEQ=0, A/B)
+            w_hh = l.weight_hh_l0
+            c = cq[0].contiguous().clone()
+            h = None
+            for t in range(T):
+                if t == 0:  # TR(h0) x TR(W_hh): term-pair
+                    hh = self._tp_linear(h0[0].contiguous(), 'hh', l.bias_hh_l0)
+                else:
+                    hh = torch.addmm(l.bias_hh_l0, h, w_hh.t())
+                tq_native.lstm_cell(gx[t], hh.contiguous(), c, out0[t])
+                h = out0[t]
+            hn, cn = [out0[T - 1]], [c]
+            out = out0
+            if self._upper is not None:
+                out, (hu, cu) = self._upper(out0, (hq[1:].contiguous(), cq[1:].contiguous()))
+                hn += list(hu)
+                cn += list(cu)
+            return out, (torch.stack(hn), torch.stack(cn))
+        # the whole recurrence of each layer in one persistent launch (tq_lstm_seq_f32);
+        # layer 0 from TR(h0), TR(c0) with the TR'd W_hh (fp32 on the TR'd values)
+        c_last = torch.empty((l.num_layers, B, H), dtype=emb.dtype, device=emb.device)
+        tq_native.lstm_seq(gx, l.weight_hh_l0.contiguous(), l.bias_hh_l0.contiguous(),
+                           hq[0].contiguous(), cq[0].contiguous(), out0, c_last[0])
+        outs = [out0]
+        if self._upper is not None and os.environ.get("TQ_LSTM_UPPER", "seq") == "miopen":
             out, (hu, cu) = self._upper(out0, (hq[1:].contiguous(), cq[1:].contiguous()))
-            hn += list(hu)
-            cn += list(cu)
-        return out, (torch.stack(hn), torch.stack(cn))
+            return out, (torch.cat([out0[T - 1:], hu]), torch.cat([c_last[:1], cu]))
+        x = out0
+        for k in range(1, l.num_layers):
+            # layers >= 1 (weights untouched by the reference): input projection over all
+            # steps as one GEMM, then the recurrence in one launch
+            w_ih = getattr(l, 'weight_ih_l%d' % k)
+            gxk = torch.addmm(getattr(l, 'bias_ih_l%d' % k), x.view(T * B, H),
+                              w_ih.t()).view(T, B, 4 * H)
+            yk = torch.empty((T, B, H), dtype=emb.dtype, device=emb.device)
+            tq_native.lstm_seq(gxk, getattr(l, 'weight_hh_l%d' % k).contiguous(),
+                               getattr(l, 'bias_hh_l%d' % k).contiguous(),
+                               hq[k].contiguous(), cq[k].contiguous(), yk, c_last[k])
+            outs.append(yk)
+            x = yk
+        hn = torch.stack([o[T - 1] for o in outs])
+        return x, (hn, c_last)
+
+    @staticmethod
+    def _seq_kernel(batch, hidden):
+        return (os.environ.get("TQ_LSTM_SEQ", "1") != "0" and hidden <= 1024 and
+                batch * hidden <= 16384)
 
     def forward(self, emb, hidden):
         if self.termpair and not self.input_quant.tracking and emb.is_cuda:

@@ -218,3 +218,21 @@ def test_fused_conv_code_rows_must_be_roundup_cout():
                                           1.0, None, p, 8, 8, ctypes.byref(epi), None)
         err = lib.tq_last_error()
         assert rc == 1 and b"roundup(cout, 8)" in err, err
+
+
+def test_lstm_seq_argument_validation():
+    """tq_lstm_seq_f32 rejects sizes outside its domain and a short workspace before any
+    launch."""
+    lib = tq_native.lib()
+    buf = torch.zeros(1 << 16, dtype=torch.float32)
+    p = buf.data_ptr()
+    rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 10, 1100, p, 1 << 20, None)
+    assert rc == 1 and b"hidden <= 1024" in lib.tq_last_error()
+    rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 100, 650, p, 1 << 20, None)
+    assert rc == 1 and b"batch * hidden" in lib.tq_last_error()
+    need = lib.tq_lstm_seq_workspace_bytes(10, 650)
+    assert need == 2 * 10 * 650 * 8
+    rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 10, 650, p, need - 8, None)
+    assert rc == 1 and b"workspace" in lib.tq_last_error()
+    rc = lib.tq_lstm_seq_f32(p, p, None, None, p, p, p, 35, 10, 650, p, need, None)
+    assert rc == 1 and b"null" in lib.tq_last_error()

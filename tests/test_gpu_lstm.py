@@ -27,9 +27,19 @@ def _oracle_w(w, bits, g, k):
     return torch.from_numpy(oracle.tr(w.detach().cpu().contiguous().numpy(), sf, bits, g, k))
 
 
-@pytest.mark.parametrize("termpair", [False, True])
-def test_lstm650_tq_chunk_against_oracle(termpair):
+@pytest.mark.parametrize("termpair,seq", [(False, None), (True, "1"), (True, "0"),
+                                          (True, "miopen")])
+def test_lstm650_tq_chunk_against_oracle(termpair, seq, monkeypatch):
+    """seq (term-pair path): "1" = each layer's recurrence in one persistent launch
+    (tq_lstm_seq_f32, both layers), "0" = per-step launches (a GEMM + tq_lstm_cell_f32 per
+    step, MIOpen for layer 1), "miopen" = the persistent launch for layer 0, MIOpen above."""
     import evaluate_lstm
+    import tq_native
+    if seq == "miopen":
+        monkeypatch.setenv("TQ_LSTM_UPPER", "miopen")
+    elif seq is not None:
+        monkeypatch.setenv("TQ_LSTM_SEQ", seq)
+    tq_native.sync_faults()
     from lstm_models.model import RNNModel
     torch.manual_seed(1111)
     model = RNNModel("LSTM", VOCAB, NHID, NHID, 2, 0.5, True).to(DEV).eval()
@@ -96,3 +106,4 @@ def test_lstm650_tq_chunk_against_oracle(termpair):
     assert float(err.max()) <= 1e-5 * float(lp_ref.abs().max()), float(err.max())
     assert float((hn.cpu().double() - hr).abs().max()) <= 1e-5
     assert float((cn.cpu().double() - cr).abs().max()) <= 1e-5 * max(1.0, float(cr.abs().max()))
+    assert tq_native.sync_faults() == 0  # no bounded step-exchange wait ran out

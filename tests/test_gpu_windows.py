@@ -199,7 +199,7 @@ def test_strip_engine_bit_identical(shape, mode, monkeypatch):
     epilogue shapes the executor uses (codes only / plain fp32; residual + fp32 + two code
     targets is not strip-eligible and must come back from the fallback unchanged)."""
     monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
-    tq_native.strip_sync_faults()  # start from a clean fault count
+    tq_native.sync_faults()  # start from a clean fault count
     n, h, w = shape
     torch.manual_seed(n * 100 + h)
     conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False)
@@ -233,7 +233,7 @@ def test_strip_engine_bit_identical(shape, mode, monkeypatch):
                 kc_steps=lay.kc_steps_nonneg)
         outs.append((o.cpu(), ca.cpu(), cb.cpu()))
     (o0, a0, b0), (o1, a1, b1) = outs
-    assert tq_native.strip_sync_faults() == 0  # no bounded team-sync wait ran out
+    assert tq_native.sync_faults() == 0  # no bounded team-sync wait ran out
     if mode != "conv1":
         assert not torch.isnan(o0).any()
         _same(o0.permute(0, 2, 3, 1), o1.permute(0, 2, 3, 1), "out")
