@@ -126,14 +126,28 @@ __global__ __launch_bounds__(kSeqThreads) void lstm_seq_kernel(LstmSeqArgs a) {
           v[k] = i < B * H ? __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                            : ((uint64_t)epoch << 32);
         }
+        // not-ready granules are re-polled together: one round trip per retry, not one per
+        // granule
+        uint32_t pending = 0;
+#pragma unroll
+        for (int k = 0; k < kSeqBatch; ++k)
+          pending |= (uint32_t)((uint32_t)(v[k] >> 32) != epoch) << k;
+        while (pending && spins_left) {
+          __builtin_amdgcn_s_sleep(2);
+          --spins_left;
+#pragma unroll
+          for (int k = 0; k < kSeqBatch; ++k)
+            if ((pending >> k) & 1u)
+              v[k] = __hip_atomic_load(g + i0 + k * kSeqThreads, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+          pending = 0;
+#pragma unroll
+          for (int k = 0; k < kSeqBatch; ++k)
+            pending |= (uint32_t)((uint32_t)(v[k] >> 32) != epoch) << k;
+        }
 #pragma unroll
         for (int k = 0; k < kSeqBatch; ++k) {
           const int i = i0 + k * kSeqThreads;
-          while ((uint32_t)(v[k] >> 32) != epoch && spins_left) {
-            __builtin_amdgcn_s_sleep(1);
-            --spins_left;
-            v[k] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
           if (i < B * H) hprev[i] = __uint_as_float((uint32_t)v[k]);
         }
       }

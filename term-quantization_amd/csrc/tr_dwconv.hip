@@ -216,15 +216,13 @@ __global__ __launch_bounds__(256) void dwconv_tp_rows_kernel(DwConvArgs a) {
   }
 }
 
-// Sliding-window 3x3 depthwise kernel (dilation 1, stride S = 1 or 2): a lane owns CPL
+// Window-blocked 3x3 depthwise kernel (dilation 1, stride S = 1 or 2): a lane owns CPL
 // channels of one output column over R consecutive output rows.  The nine taps' weights stay
-// in registers for all R rows; the input rows are a window of three tap rows (each the three
-// column taps, CPL codes apiece) that slides down by S rows per output row, and the S rows
-// the next output row adds are loaded while the current one computes and runs its epilogue:
-// every input row is loaded once per lane (S + (3 - S) / R rows per output instead of 3 per
-// output and 9 loads), and the loads stream with no round trip of their own.  Taps in the
-// padding read a zero block (unconditional loads).  Lanes run chunk-fastest, then along the
-// output row, so a wave's load of one tap covers contiguous NHWC bytes.
+// in registers for all R rows, and the (R - 1) S + 3 input rows of the block (each the three
+// column taps, CPL codes apiece) are all loaded up front, so every input row is loaded once
+// per lane and a lane keeps ~30 loads in flight (the kernel is bound by bytes in flight).
+// Taps in the padding read a zero block (unconditional loads).  Lanes run chunk-fastest,
+// then along the output row, so a wave's load of one tap covers contiguous NHWC bytes.
 template <int S, int R, int CPL>
 __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
@@ -275,17 +273,14 @@ __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
   };
   const uint16_t* l = a.lut_c ? lut : nullptr;
   const int ih0 = oh0 * S - a.ph;  // first tap row of output row oh0
-  v4i win[3][3];
+  // every input row of the block's window is issued up front (NROW x 3 loads in flight per
+  // lane: the bytes in flight, not the VALU, bound this kernel), then the rows are consumed
+  constexpr int NROW = (R - 1) * S + 3;
+  v4i rows[NROW][3];
 #pragma unroll
-  for (int kr = 0; kr < 3; ++kr) load_row(ih0 + kr, win[kr]);
+  for (int k = 0; k < NROW; ++k) load_row(ih0 + k, rows[k]);
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    // the S new tap rows of output row j + 1, in flight during row j's MACs and epilogue
-    v4i nxt[S][3];
-    if (j + 1 < R) {
-#pragma unroll
-      for (int u = 0; u < S; ++u) load_row(ih0 + (j + 1) * S + 3 - S + u, nxt[u]);
-    }
     int acc[CPL];
 #pragma unroll
     for (int i = 0; i < CPL; ++i) acc[i] = 0;
@@ -293,7 +288,7 @@ __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
     for (int kr = 0; kr < 3; ++kr)
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) {
-        const v4i xv = win[kr][ks];
+        const v4i xv = rows[j * S + kr][ks];
 #pragma unroll
         for (int i = 0; i < CPL / 2; ++i) {
           const int lo = (int)(short)(xv[i] & 0xFFFF);
@@ -305,13 +300,6 @@ __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
     const int oh = oh0 + j;
     if (oh < a.Ho)
       dw_emit<CPL>(a, l, (img * a.Ho + oh) * a.Wo + ow, img, oh * a.Wo + ow, c0, acc);
-    if (j + 1 < R) {
-#pragma unroll
-      for (int kr = 0; kr < 3; ++kr)
-#pragma unroll
-        for (int ks = 0; ks < 3; ++ks)
-          win[kr][ks] = kr + S < 3 ? win[kr + S][ks] : nxt[kr + S - 3][ks];
-    }
   }
 }
 
@@ -327,17 +315,18 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   const int slide = slide_env ? atoi(slide_env) : 4;
   if (slide && !(rows_env && atoi(rows_env) == 0) && a.KH == 3 && a.KW == 3 && a.dh == 1 &&
       a.dw == 1 && a.sh == a.sw && (a.sh == 1 || a.sh == 2) && a.Cp % slide == 0) {
-    constexpr int R = 8;
-    const int cpl = slide == 4 ? 4 : 8;
+    // rows per lane: 8 at stride 1 (10 input rows in flight), 4 at stride 2 (9 rows)
+    const int R = a.sh == 1 ? 8 : 4;
+    const int cpl = slide == 8 ? 8 : 4;
     const int64_t lanes = (int64_t)a.N * ((a.Ho + R - 1) / R) * a.Wo * (a.Cp / cpl);
     const dim3 grid((unsigned)((lanes + 255) / 256));
     const size_t lds = (size_t)a.lut_c * 2;
     if (cpl == 8) {
-      if (a.sh == 1) dwconv3_slide_kernel<1, R, 8><<<grid, 256, lds, stream>>>(a);
-      else dwconv3_slide_kernel<2, R, 8><<<grid, 256, lds, stream>>>(a);
+      if (a.sh == 1) dwconv3_slide_kernel<1, 8, 8><<<grid, 256, lds, stream>>>(a);
+      else dwconv3_slide_kernel<2, 4, 8><<<grid, 256, lds, stream>>>(a);
     } else {
-      if (a.sh == 1) dwconv3_slide_kernel<1, R, 4><<<grid, 256, lds, stream>>>(a);
-      else dwconv3_slide_kernel<2, R, 4><<<grid, 256, lds, stream>>>(a);
+      if (a.sh == 1) dwconv3_slide_kernel<1, 8, 4><<<grid, 256, lds, stream>>>(a);
+      else dwconv3_slide_kernel<2, 4, 4><<<grid, 256, lds, stream>>>(a);
     }
     return hipGetLastError();
   }
