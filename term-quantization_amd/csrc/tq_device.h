@@ -164,6 +164,55 @@ __device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
   return (uint32_t)r + (__builtin_amdgcn_fractf(r) >= 0.5f ? 1u : 0u);
 }
 
+// Epilogue arithmetic of the term-pair kernels (TQ_EPI_F32, default 1: fp32).
+//   fold_acc: y = fp32(acc * sc + sh) of the exact integer sum -- in fp32 (one fma of the
+//     int -> fp32 converted sum, |error| <= ~3 ulp of max(|acc sc|, |y|), far inside the 1e-5
+//     parity bound) instead of fp64 (6 fp64-rate operations per value); every engine uses the
+//     same fold, so their outputs stay bit-identical.
+//   relu_q_epi: relu_q (q = round(fp32(y / sf)), exact as the reference rounds) from an fp32
+//     product y * fp32(1/sf): |r_fast - fp32(y / sf)| <= 3 * 2^-24 r, so the rounded integer
+//     can differ only when r_fast lies within that of a half-integer; those values (about
+//     one in 4000) take the exact fp64 quotient.  The codes are TR of the stored y either way.
+#ifndef TQ_EPI_F32
+#define TQ_EPI_F32 1
+#endif
+#if TQ_EPI_F32
+typedef float coef_t;
+__device__ __forceinline__ float fold_acc(int acc, float sc, float sh) {
+  return fmaf((float)acc, sc, sh);
+}
+// N values at once: one (rare) exact fallback block for the group
+template <int N>
+__device__ __forceinline__ void relu_q_epi(const float* y, double inv_sf, float maxv,
+                                           uint32_t* q) {
+  const float inv = (float)inv_sf;
+  bool near = false;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float r = fminf(y[i] * inv, maxv + 1.0f);  // y >= 0, not NaN (after ReLU)
+    const float fr = __builtin_amdgcn_fractf(r);
+    const uint32_t qi = (uint32_t)r + (fr >= 0.5f ? 1u : 0u);
+    q[i] = qi < (uint32_t)maxv ? qi : (uint32_t)maxv;
+    near |= fabsf(fr - 0.5f) <= r * 0x1p-21f;
+  }
+  if (__builtin_expect(near, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = relu_q(y[i], inv_sf, maxv);
+  }
+}
+#else
+typedef double coef_t;
+__device__ __forceinline__ float fold_acc(int acc, double sc, double sh) {
+  return (float)((double)acc * sc + sh);
+}
+template <int N>
+__device__ __forceinline__ void relu_q_epi(const float* y, double inv_sf, float maxv,
+                                           uint32_t* q) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) q[i] = relu_q(y[i], inv_sf, maxv);
+}
+#endif
+
 // Fused-epilogue activation (DwConvArgs relu, tq_act_encode_act): 0 none, 1 ReLU, 2 ReLU6,
 // 3 swish y * sigmoid(y) (EfficientNet's MemoryEfficientSwish, with torch's fp32 sigmoid
 // 1 / (1 + exp(-y))).  y becomes the value the next layer's codes encode, o the stored value:

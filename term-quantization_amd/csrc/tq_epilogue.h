@@ -16,17 +16,17 @@ namespace tq {
 namespace {
 
 // Per-channel epilogue coefficients of channels co..co+3: y = acc * sc + sh (fp64).
-__device__ __forceinline__ void load_coef(const ConvArgs& a, int co, double sc[4],
-                                          double sh[4]) {
+__device__ __forceinline__ void load_coef(const ConvArgs& a, int co, coef_t sc[4],
+                                          coef_t sh[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const bool ok = co + i < a.Cout;
     if (a.ch_scale) {
-      sc[i] = ok ? a.ch_scale[co + i] : 0.0;
-      sh[i] = ok ? a.ch_shift[co + i] : 0.0;
+      sc[i] = (coef_t)(ok ? a.ch_scale[co + i] : 0.0);
+      sh[i] = (coef_t)(ok ? a.ch_shift[co + i] : 0.0);
     } else {
-      sc[i] = a.scale;
-      sh[i] = (a.bias && ok) ? (double)a.bias[co + i] : 0.0;
+      sc[i] = (coef_t)a.scale;
+      sh[i] = (coef_t)((a.bias && ok) ? (double)a.bias[co + i] : 0.0);
     }
   }
 }
@@ -41,8 +41,10 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, i
                                              const uint16_t* lut = nullptr) {
   uint32_t v[4];
   if (lut) {  // the fast path's codes from the LDS table (set only where it applies)
+    uint32_t qv[4];
+    relu_q_epi<4>(y, inv_sf, maxv, qv);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = lut[relu_q(y[i], inv_sf, maxv)];
+    for (int i = 0; i < 4; ++i) v[i] = lut[qv[i]];
   } else if (relu && inv_sf > 0.0 && inv_sf <= 1.0e308) {  // y >= 0, 0 < sf < inf: fast path
     int32_t t[4];
     tr_values_relu4(y, inv_sf, maxv, relu_peels(maxv, k), t);
@@ -66,13 +68,13 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, i
 // strip and register-staged engines' epilogue arrays in scratch).
 template <bool SWISH = false>
 __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int co,
-                                               const int acc[4], const double sc[4],
-                                               const double sh[4], const float4 rv,
+                                               const int acc[4], const coef_t sc[4],
+                                               const coef_t sh[4], const float4 rv,
                                                const uint16_t* lut_a = nullptr,
                                                const uint16_t* lut_b = nullptr) {
   float y[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
+  for (int i = 0; i < 4; ++i) y[i] = fold_acc(acc[i], sc[i], sh[i]);
   if (a.residual || a.ds_x) {
     y[0] += rv.x;
     y[1] += rv.y;
@@ -104,13 +106,13 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
 // one fp64->fp32 rounding, residual add and ReLU in fp32, fp32 store, next layers' TR codes
 // (tr_layer.py:96-99 applied to the stored value).
 __device__ __forceinline__ void emit4_nhwc(const ConvArgs& a, int64_t p, int co,
-                                           const int acc[4], const double sc[4],
-                                           const double sh[4], bool vec,
+                                           const int acc[4], const coef_t sc[4],
+                                           const coef_t sh[4], bool vec,
                                            const uint16_t* lut_a = nullptr,
                                            const uint16_t* lut_b = nullptr) {
   float y[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = (float)((double)acc[i] * sc[i] + sh[i]);
+  for (int i = 0; i < 4; ++i) y[i] = fold_acc(acc[i], sc[i], sh[i]);
   if (a.residual) {
     const float* r = a.residual + p * a.Cout + co;
     if (vec) {

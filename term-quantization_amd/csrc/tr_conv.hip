@@ -182,7 +182,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int64_t
     for (int h = 0; h < 2; ++h) {
       const int co = m0 + h * (BM / 2) + ty * 4;
       if (co >= a.Cout) continue;
-      double sc[4], sh[4];
+      coef_t sc[4], sh[4];
       load_coef(a, co, sc, sh);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -200,14 +200,14 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int64_t
     for (int i = 0; i < 8; ++i) {
       const int co = m0 + (i < 4 ? ty * 4 + i : BM / 2 + ty * 4 + (i - 4));
       if (co >= a.Cout) continue;
-      const double sc = a.scale;
-      const double sh = a.bias ? (double)a.bias[co] : 0.0;
+      const coef_t sc = (coef_t)a.scale;
+      const coef_t sh = (coef_t)(a.bias ? (double)a.bias[co] : 0.0);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int64_t p0 = n0 + h * (BN / 2) + tx * 4;
         float y[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = (float)((double)acc[i][h * 4 + j] * sc + sh);
+        for (int j = 0; j < 4; ++j) y[j] = fold_acc(acc[i][h * 4 + j], sc, sh);
         if (vec && p0 + 3 < a.P) {
           const int64_t img = p0 / HoWo;
           *reinterpret_cast<float4*>(a.out + (img * a.Cout + co) * HoWo + (p0 - img * HoWo)) =
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void conv_finalize_kernel(ConvArgs a) {
   const int co = (int)(t - p * groups) * 4;
   const int4 s = *reinterpret_cast<const int4*>(a.ws + p * a.Cout + co);
   const int acc4[4] = {s.x, s.y, s.z, s.w};
-  double sc[4], sh[4];
+  coef_t sc[4], sh[4];
   load_coef(a, co, sc, sh);
   emit4_nhwc(a, p, co, acc4, sc, sh, true);
 }

@@ -307,20 +307,20 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     // the identity: fp32(acc2 * ds_scale + ds_shift), as the separate downsample conv stores it
     put_tile(true);
     if (co < a.Cout) {
-      double sc2[4], sh2[4];
+      coef_t sc2[4], sh2[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        sc2[i] = coef2[4 * slot + i][0];
-        sh2[i] = coef2[4 * slot + i][1];
+        sc2[i] = (coef_t)coef2[4 * slot + i][0];
+        sh2[i] = (coef_t)coef2[4 * slot + i][1];
       }
 #pragma unroll
       for (int it = 0; it < 32 / PXI; ++it) {
         const int px = it * PXI + lane / C::SL;
         const u32x4 v = t[px * C::SL + (slot ^ (px & 15))];
-        res[it] = make_float4((float)((double)(int)v.x * sc2[0] + sh2[0]),
-                              (float)((double)(int)v.y * sc2[1] + sh2[1]),
-                              (float)((double)(int)v.z * sc2[2] + sh2[2]),
-                              (float)((double)(int)v.w * sc2[3] + sh2[3]));
+        res[it] = make_float4(fold_acc((int)v.x, sc2[0], sh2[0]),
+                              fold_acc((int)v.y, sc2[1], sh2[1]),
+                              fold_acc((int)v.z, sc2[2], sh2[2]),
+                              fold_acc((int)v.w, sc2[3], sh2[3]));
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // every read of the tile has returned
@@ -328,11 +328,11 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   }
   put_tile(false);
   if (co >= a.Cout) return;
-  double sc[4], sh[4];
+  coef_t sc[4], sh[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    sc[i] = coef[4 * slot + i][0];
-    sh[i] = coef[4 * slot + i][1];
+    sc[i] = (coef_t)coef[4 * slot + i][0];
+    sh[i] = (coef_t)coef[4 * slot + i][1];
   }
   // fully unrolled: res[] must stay in registers (a partial unroll indexes it in scratch)
 #pragma clang loop unroll(full)

@@ -195,7 +195,7 @@ __device__ __forceinline__ void mfma_epilogue(const ConvArgs& a, int m0, int64_t
       for (int q = 0; q < 4; ++q) {
         const int co = m0 + wm + 32 * bm + 8 * q + 4 * hh;
         if (co >= a.Cout) continue;
-        double sc[4], sh[4];
+        coef_t sc[4], sh[4];
         load_coef(a, co, sc, sh);
 #pragma unroll
         for (int bn = 0; bn < 2; ++bn) {
@@ -221,9 +221,9 @@ __device__ __forceinline__ void mfma_epilogue(const ConvArgs& a, int m0, int64_t
         for (int r = 0; r < 16; ++r) {
           const int co = m0 + wm + 32 * bm + 8 * (r >> 2) + 4 * hh + (r & 3);
           if (co >= a.Cout) continue;
-          const double sh = a.bias ? (double)a.bias[co] : 0.0;
+          const coef_t sh = (coef_t)(a.bias ? (double)a.bias[co] : 0.0);
           a.out[(img * a.Cout + co) * HoWo + rem] =
-              (float)((double)acc.i[bm][bn][r] * a.scale + sh);
+              fold_acc(acc.i[bm][bn][r], (coef_t)a.scale, sh);
         }
     }
   }
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(pipe_threads(BM, BN), 1) void conv2d_tp_mfma_pipe_k
   const int slot = lane & 15;
   const int co = m0 + wm + 4 * slot;
   if (co < a.Cout) {
-    double sc[4], sh[4];
+    coef_t sc[4], sh[4];
     load_coef(a, co, sc, sh);
 #pragma unroll 4
     for (int it = 0; it < 16; ++it) {

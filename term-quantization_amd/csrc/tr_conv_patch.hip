@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kPatchThreads, MB == 1 ? 4 : 2) void conv2d_tp_patc
     const int slot = lane % SLOTS;
     const int co = m0 + wm + 4 * slot;
     if (co < a.Cout) {
-      double sc[4], sh[4];
+      coef_t sc[4], sh[4];
       load_coef(a, co, sc, sh);
       constexpr int PXI = 64 / SLOTS;  // pixels per wave-instruction
 #pragma unroll 4

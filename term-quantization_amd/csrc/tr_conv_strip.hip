@@ -107,7 +107,7 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
   float y[4], o[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    y[e] = (float)((double)(int)acc4[e] * ep.sc + ep.sh);
+    y[e] = fold_acc((int)acc4[e], (coef_t)ep.sc, (coef_t)ep.sh);
     if (RES) y[e] += rv[e];  // (no + 0.0f without one: -0.0 stays, as in tq_epilogue.h)
     o[e] = y[e];
     if (a.relu) {
@@ -131,8 +131,10 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
     const int fmt = side ? a.fmt_b : a.fmt_a;
     uint32_t bits[4];
     if (lut) {  // the ReLU fast path's codes from the LDS table
+      uint32_t qv[4];
+      relu_q_epi<4>(y, inv, maxv, qv);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bits[e] = lut[relu_q(y[e], inv, maxv)];
+      for (int e = 0; e < 4; ++e) bits[e] = lut[qv[e]];
     } else {
       int32_t v[4];
       if (side ? ep.fast_b : ep.fast_a) {

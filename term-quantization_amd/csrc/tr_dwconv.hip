@@ -36,10 +36,10 @@ __device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut
   for (int i = 0; i < CPL; ++i) {
     const int c = c0 + i;
     if (a.ch_scale) {  // folded BN (pad channels: 0)
-      y[i] = c < a.C ? (float)((double)acc[i] * a.ch_scale[c] + a.ch_shift[c]) : 0.0f;
+      y[i] = c < a.C ? fold_acc(acc[i], (coef_t)a.ch_scale[c], (coef_t)a.ch_shift[c]) : 0.0f;
     } else {
       const double sh = (a.bias && c < a.C) ? (double)a.bias[c] : 0.0;
-      y[i] = (float)((double)acc[i] * a.scale + sh);
+      y[i] = fold_acc(acc[i], (coef_t)a.scale, (coef_t)sh);
     }
   }
   const bool full = (a.C % CPL) == 0;
@@ -65,8 +65,10 @@ __device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut
   if (a.codes) {  // next layer's codes of channels c0 .. c0 + CPL - 1 (cp_c == Cp)
     uint32_t v[CPL];
     if (a.lut_c) {
+      uint32_t qv[CPL];
+      relu_q_epi<CPL>(y, a.inv_c, a.maxv_c, qv);
 #pragma unroll
-      for (int i = 0; i < CPL; ++i) v[i] = lut[relu_q(y[i], a.inv_c, a.maxv_c)];
+      for (int i = 0; i < CPL; ++i) v[i] = lut[qv[i]];
     } else {
 #pragma unroll
       for (int i = 0; i < CPL; ++i)
