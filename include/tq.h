@@ -43,10 +43,9 @@ const char *tq_last_error(void);
 
 /*
  * Diagnostics: the number of bounded in-kernel waits that ran out since the previous call --
- * the row-strip conv engine's team syncs and tq_lstm_seq_f32's step exchange (each one means
- * a launch went on without confirming data it waited for, so its results are suspect) --
- * then clears the count.  Synchronous (waits for the device); `count` is a host pointer.  A
- * healthy run reads 0.
+ * the row-strip conv engine's team syncs (each one means a launch went on without confirming
+ * that its LDS patch was staged, so its results are suspect) -- then clears the count.
+ * Synchronous (waits for the device); `count` is a host pointer.  A healthy run reads 0.
  */
 int tq_sync_faults(uint32_t *count);
 
@@ -377,15 +376,16 @@ int tq_lstm_cell_f32(const float *gx, const float *hh, float *c, float *h, int64
 
 /*
  * A whole LSTM layer's recurrence (torch.nn.LSTM semantics, gate order i, f, g, o) in one
- * persistent launch, replacing T x (a recurrent-projection GEMM + tq_lstm_cell_f32) of
- * TRLSTMLayer's per-step loop (tr_layer.py:191-195 runs cuDNN's LSTM there):
+ * call, replacing T x (a recurrent-projection GEMM + tq_lstm_cell_f32) of TRLSTMLayer's
+ * per-step loop (tr_layer.py:191-195 runs cuDNN's LSTM there): T fused step launches,
  *   gates_t = gx[t] + b_hh + h_{t-1} W_hh^T,  c_t = sigmoid(f) c_{t-1} + sigmoid(i) tanh(g),
  *   h_t = sigmoid(o) tanh(c_t),  out[t] = h_t,  for t < steps, from (h0, c0)
  * gx [steps][batch][4 hidden] (the input projection incl. b_ih), w_hh [4 hidden][hidden],
  * b_hh [4 hidden] (or NULL), h0/c0/c_out [batch][hidden], out [steps][batch][hidden], all fp32
- * device buffers; c_out = c_{steps-1} (h_{steps-1} is out[steps-1]).  `workspace` >=
- * tq_lstm_seq_workspace_bytes(batch, hidden) device bytes, zeroed by the call (enqueued).
- * Domain: hidden <= 1024, batch * hidden <= 16384.  fp32 arithmetic, a fixed summation order.
+ * device buffers; c_out = c_{steps-1} (h_{steps-1} is out[steps-1]); out and c_out may not
+ * alias h0 / c0.  `workspace`: tq_lstm_seq_workspace_bytes(batch, hidden) device bytes (0 in
+ * this version).  Domain: hidden <= 1024, batch * hidden <= 16384.  fp32 arithmetic, a fixed
+ * summation order.
  */
 int64_t tq_lstm_seq_workspace_bytes(int64_t batch, int64_t hidden);
 int tq_lstm_seq_f32(const float *gx, const float *w_hh, const float *b_hh, const float *h0,

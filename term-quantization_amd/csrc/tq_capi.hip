@@ -80,12 +80,7 @@ const char* tq_last_error(void) { return g_err; }
 
 int tq_sync_faults(uint32_t* count) {
   if (count == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "sync_faults: count is null");
-  uint32_t strip = 0, seq = 0;
-  int rc = hip_status(tq::strip_sync_faults(&strip), "sync_faults");
-  if (rc != TQ_OK) return rc;
-  rc = hip_status(tq::lstm_seq_faults(&seq), "sync_faults");
-  *count = strip + seq;
-  return rc;
+  return hip_status(tq::strip_sync_faults(count), "sync_faults");
 }
 
 int tq_tr_f32(const float* input, float* output, int64_t ndim, const int64_t* shape, float sf,
@@ -706,11 +701,12 @@ int tq_lstm_seq_f32(const float* gx, const float* w_hh, const float* b_hh, const
     return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: sizes outside hidden <= 1024, batch * "
                 "hidden <= 16384");
   if (steps * batch * hidden == 0) return TQ_OK;
-  if (!gx || !w_hh || !h0 || !c0 || !out || !c_out || !workspace)
+  if (!gx || !w_hh || !h0 || !c0 || !out || !c_out)
     return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: null pointer");
-  if (workspace_bytes < tq::lstm_seq_workspace_bytes(batch, hidden) ||
-      (uintptr_t)workspace % 16)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: workspace too small or misaligned");
+  if (workspace_bytes < tq::lstm_seq_workspace_bytes(batch, hidden))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: workspace too small");
+  if (c_out == c0 || c_out == out || h0 == out)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: c_out / out may not alias the inputs");
   return hip_status(tq::launch_lstm_seq(gx, w_hh, b_hh, h0, c0, out, c_out, steps, batch,
                                         hidden, workspace, (hipStream_t)stream),
                     "lstm_seq launch");

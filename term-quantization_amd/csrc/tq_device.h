@@ -174,7 +174,7 @@ __device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
 //     can differ only when r_fast lies within that of a half-integer; those values (about
 //     one in 4000) take the exact fp64 quotient.  The codes are TR of the stored y either way.
 #ifndef TQ_EPI_F32
-#define TQ_EPI_F32 1
+#define TQ_EPI_F32 0
 #endif
 #if TQ_EPI_F32
 typedef float coef_t;

@@ -106,13 +106,12 @@ hipError_t launch_conv2d_wide(const WideConvArgs& a, hipStream_t stream);
 // LSTM cell update (tq_lstm.hip): c, h [B][H] in place / out from gx, hh [B][4H]
 hipError_t launch_lstm_cell(const float* gx, const float* hh, float* c, float* h, int64_t B,
                             int64_t H, hipStream_t stream);
-// A whole LSTM layer's recurrence in one persistent launch (tq_lstm.hip)
+// A whole LSTM layer's recurrence: T fused step launches from one call (tq_lstm.hip)
 int64_t lstm_seq_workspace_bytes(int64_t B, int64_t H);
 hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, const float* h0,
                            const float* c0, float* out, float* cT, int64_t T, int64_t B,
                            int64_t H, void* ws, hipStream_t stream);
-// reads and clears the LSTM step exchange's fault counter (synchronous)
-hipError_t lstm_seq_faults(uint32_t* count);
+
 
 struct PoolArgs {
   const float* x;        // [N][H][W][C] fp32 (channels_last), C % 8 == 0

@@ -471,8 +471,8 @@ class TRLSTMLayer(nn.Module):
                 hn += list(hu)
                 cn += list(cu)
             return out, (torch.stack(hn), torch.stack(cn))
-        # the whole recurrence of each layer in one persistent launch (tq_lstm_seq_f32);
-        # layer 0 from TR(h0), TR(c0) with the TR'd W_hh (fp32 on the TR'd values)
+        # each layer's recurrence in one call (tq_lstm_seq_f32: a fused step kernel per
+        # step); layer 0 from TR(h0), TR(c0) with the TR'd W_hh (fp32 on the TR'd values)
         c_last = torch.empty((l.num_layers, B, H), dtype=emb.dtype, device=emb.device)
         tq_native.lstm_seq(gx, l.weight_hh_l0.contiguous(), l.bias_hh_l0.contiguous(),
                            hq[0].contiguous(), cq[0].contiguous(), out0, c_last[0])
@@ -483,7 +483,7 @@ class TRLSTMLayer(nn.Module):
         x = out0
         for k in range(1, l.num_layers):
             # layers >= 1 (weights untouched by the reference): input projection over all
-            # steps as one GEMM, then the recurrence in one launch
+            # steps as one GEMM, then the recurrence in one call
             w_ih = getattr(l, 'weight_ih_l%d' % k)
             gxk = torch.addmm(getattr(l, 'bias_ih_l%d' % k), x.view(T * B, H),
                               w_ih.t()).view(T, B, 4 * H)

@@ -231,8 +231,11 @@ def test_lstm_seq_argument_validation():
     rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 100, 650, p, 1 << 20, None)
     assert rc == 1 and b"batch * hidden" in lib.tq_last_error()
     need = lib.tq_lstm_seq_workspace_bytes(10, 650)
-    assert need == 2 * 10 * 650 * 8
+    assert need == 0
     rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 10, 650, p, need - 8, None)
     assert rc == 1 and b"workspace" in lib.tq_last_error()
     rc = lib.tq_lstm_seq_f32(p, p, None, None, p, p, p, 35, 10, 650, p, need, None)
     assert rc == 1 and b"null" in lib.tq_last_error()
+    q = p + 4096
+    rc = lib.tq_lstm_seq_f32(p, p, None, p, q, p + 8192, q, 35, 10, 650, None, 0, None)
+    assert rc == 1 and b"alias" in lib.tq_last_error()
