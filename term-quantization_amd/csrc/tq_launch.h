@@ -168,6 +168,8 @@ bool conv_patch_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_patch(const ConvArgs& a, int mb, hipStream_t stream);
 // MFMA direct engine (tr_conv_direct.hip): Cp % 64 == 0, NHWC out; mb = 1 (64 x 128 tiles)
 // or 2 (128 x 128 tiles).
+bool conv_pw_eligible(const ConvArgs& a, int out_nhwc);
+hipError_t launch_conv2d_pw(const ConvArgs& a, hipStream_t stream);
 bool conv_direct_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream);
 // MFMA row-strip engine (tr_conv_strip.hip): 3x3 stride-1 pad-1 convs with 64 -> 64 channels,

@@ -349,6 +349,183 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Pointwise engine: 1x1 convs (pad 0, any stride) with K <= 4 K-steps (Cin <= 256): the
+// MobileNet-V2 / EfficientNet expand and project convs and the ResNet downsamples.  Their
+// tiles are mostly epilogue (1-4 K-steps of MFMA, then 8192 outputs), so one tile per
+// workgroup leaves each workgroup's lifetime to fixed latencies (weight DMA, fragment loads,
+// one barrier, the epilogue's stores) -- ~50k such workgroups for a 112x112 MobileNet-V2
+// layer.  Here a persistent workgroup owns one 64-row Cout tile: its weights (all NKS
+// K-steps), epilogue coefficients and code tables are staged once, and its 4 waves walk pixel
+// tiles independently (no workgroup barrier in the loop: the weights are static and each
+// wave transposes its own epilogue tile), each loading the NEXT tile's activation fragments
+// into registers before running the current tile's MFMAs and epilogue.
+// Same exact sums (no flush: the host window check covers K <= 4 steps or the kernel is not
+// used) and the same shared epilogue as the direct engine: bit-identical outputs.
+// ---------------------------------------------------------------------------------------
+constexpr int kPwWaves = 4;
+
+template <int NKS, bool SWISH>
+__global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_pw_kernel(ConvArgs a, int G) {
+  using C = DirCfg<1>;
+  __shared__ __attribute__((aligned(16))) u32x4 wlds[NKS * C::SLOT];  // [NKS][64 rows][8]
+  __shared__ __attribute__((aligned(16))) u32x4 tlds[kPwWaves * C::TILE];
+  __shared__ double coef[C::BM][2];
+  extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lut[];
+  uint16_t *lut_a, *lut_b;
+  conv_luts(a, dyn_lut, lut_a, lut_b);
+
+  const int mt = (a.Cout + C::BM - 1) / C::BM;
+  const int m0 = (blockIdx.x % mt) * C::BM;
+  const int g = blockIdx.x / mt;
+  const int64_t ntn = (a.P + C::BN - 1) / C::BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r32 = lane & 31;
+  const int hh = lane >> 5;
+  const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
+  const uint16_t* __restrict__ wg = reinterpret_cast<const uint16_t*>(a.w);
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page) + 8 * hh;
+
+  // the Cout tile's weights, every K-step, once (the swizzled image of the direct engine)
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int i = 0; i < C::AI; ++i) {
+      const int r = (wave * C::AI + i) * 8 + (lane >> 3);
+      glds16(wg + (int64_t)(m0 + r) * a.Kp + ks * kKStep + ((lane & 7) ^ ((r >> 1) & 7)) * 8,
+             wlds + ks * C::SLOT + (wave * C::AI + i) * 64);
+    }
+  for (int i = threadIdx.x; i < C::BM; i += kDirThreads) {
+    const int co = m0 + i;
+    const bool ok = co < a.Cout;
+    coef[i][0] = a.ch_scale ? (ok ? a.ch_scale[co] : 0.0) : a.scale;
+    coef[i][1] = a.ch_scale ? (ok ? a.ch_shift[co] : 0.0)
+                            : ((a.bias && ok) ? (double)a.bias[co] : 0.0);
+  }
+  TQ_WAIT_VM(0);
+  __syncthreads();  // weights, coefficients and code tables visible; no barrier after this
+
+  // epilogue role of this lane: channels m0 + 4 slot .. +3 of pixels it * PXI + lane / SL
+  constexpr int PXI = 64 / C::SL;
+  const int slot = lane % C::SL;
+  const int co = m0 + 4 * slot;
+  coef_t sc[4], sh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sc[i] = (coef_t)coef[4 * slot + i][0];
+    sh[i] = (coef_t)coef[4 * slot + i][1];
+  }
+  const bool vec = (a.Cout & 3) == 0;
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  u32x4* t = tlds + wave * C::TILE;
+
+  // activation fragments of pixel tile nt for this lane (MFMA column r32), all K-steps
+  auto load_b = [&](int64_t nt, u32x4 (&b)[NKS][4]) __attribute__((always_inline)) {
+    const int64_t p = nt * C::BN + wave * 32 + r32;
+    const uint16_t* src = zero;
+    if (p < a.P) {
+      const int64_t img = p / HoWo;
+      const int64_t rem = p - img * HoWo;
+      const int oh = (int)(rem / a.Wo);
+      const int ow = (int)(rem - (int64_t)oh * a.Wo);
+      src = xg + ((img * a.H + (int64_t)oh * a.sh) * a.W + (int64_t)ow * a.sw) * a.Cp + 8 * hh;
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int cleft = a.Cp - ks * kKStep - 8 * hh;  // codes left in this K-step's groups
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        b[ks][s4] = *reinterpret_cast<const u32x4*>(
+            (p < a.P && 16 * s4 < cleft ? src + ks * kKStep : zero) + 16 * s4);
+    }
+  };
+  auto tile = [&](int64_t nt, const u32x4 (&b)[NKS][4]) __attribute__((always_inline)) {
+    const int64_t wn0 = nt * C::BN + wave * 32;
+    float4 res[32 / PXI];  // residuals first: their latency overlaps the MFMAs
+#pragma unroll
+    for (int it = 0; it < 32 / PXI; ++it) {
+      const int64_t p = wn0 + it * PXI + lane / C::SL;
+      res[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vec && a.residual && co < a.Cout && p < a.P)
+        res[it] = *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co);
+    }
+    float16v acc[2];
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[bm][r] = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const half8 bf = __builtin_bit_cast(half8, b[ks][k]);
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm) {
+          const half8 af =
+              __builtin_bit_cast(half8, wlds[ks * C::SLOT + swz(32 * bm + r32, 2 * k + hh)]);
+          acc[bm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[bm], 0, 0, 0);
+        }
+      }
+    // int32 tile -> this wave's LDS region, transposed so a lane reads 4-channel quads
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int sl = 8 * bm + 2 * q + hh;
+        u32x4 v;
+        v.x = (uint32_t)(int)acc[bm][4 * q];
+        v.y = (uint32_t)(int)acc[bm][4 * q + 1];
+        v.z = (uint32_t)(int)acc[bm][4 * q + 2];
+        v.w = (uint32_t)(int)acc[bm][4 * q + 3];
+        t[r32 * C::SL + (sl ^ (r32 & 15))] = v;
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
+    __builtin_amdgcn_wave_barrier();
+    if (co < a.Cout) {
+#pragma clang loop unroll(full)
+      for (int it = 0; it < 32 / PXI; ++it) {
+        const int px = it * PXI + lane / C::SL;
+        const int64_t p = wn0 + px;
+        if (p >= a.P) continue;
+        const u32x4 v = t[px * C::SL + (slot ^ (px & 15))];
+        const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+        if (vec)
+          emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
+        else
+          emit4_nhwc(a, p, co, acc4, sc, sh, false, lut_a, lut_b);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // every read of the tile returned before it is reused
+    __builtin_amdgcn_wave_barrier();
+  };
+  // pixel tiles g, g + G, ...: the next tile's fragments are in flight during this one
+  u32x4 b0[NKS][4], b1[NKS][4];
+  int64_t nt = g;
+  if (nt < ntn) load_b(nt, b0);
+  for (; nt < ntn; nt += 2 * (int64_t)G) {
+    if (nt + G < ntn) load_b(nt + G, b1);
+    tile(nt, b0);
+    if (nt + G >= ntn) break;
+    if (nt + 2 * (int64_t)G < ntn) load_b(nt + 2 * (int64_t)G, b0);
+    tile(nt + G, b1);
+  }
+}
+
+template <int NKS, bool SWISH>
+hipError_t launch_pw_cfg(const ConvArgs& a, hipStream_t stream) {
+  using C = DirCfg<1>;
+  const int mt = (int)((a.Cout + C::BM - 1) / C::BM);
+  const int64_t ntn = (a.P + C::BN - 1) / C::BN;
+  // persistent: about 2 workgroups per CU in all (the register budget of 2 waves per SIMD)
+  int64_t G = (2 * (int64_t)device_cus() + mt - 1) / mt;
+  if (G > ntn) G = ntn;
+  if (G < 1) G = 1;
+  conv2d_tp_pw_kernel<NKS, SWISH>
+      <<<dim3((unsigned)(G * mt)), kDirThreads, (size_t)conv_lut_bytes(a), stream>>>(a, (int)G);
+  return hipGetLastError();
+}
+
 template <int MB, bool FLUSH, bool DS, bool SWISH = false>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   using C = DirCfg<MB>;
@@ -373,6 +550,26 @@ bool conv_direct_eligible(const ConvArgs& a, int out_nhwc) {
   return out_nhwc && (a.Cp % kKStep == 0 || (a.KH * a.KW == 1 && a.Cp % 8 == 0)) &&
          a.KH * a.KW <= 64 && a.Kp % kKStep == 0 &&
          (a.ds_x == nullptr || a.ds_Cp % kKStep == 0);
+}
+
+// The pointwise engine's shapes: 1x1, pad 0, K <= 3 K-steps (4 spills) with no flush,
+// no fused downsample.
+bool conv_pw_eligible(const ConvArgs& a, int out_nhwc) {
+  const int nks = a.Kp / kKStep;
+  return out_nhwc && a.KH == 1 && a.KW == 1 && a.ph == 0 && a.pw == 0 && a.Cp % 8 == 0 &&
+         a.Kp % kKStep == 0 && nks >= 1 && nks <= 3 &&
+         (a.kc_steps == 0 || a.kc_steps >= nks) && a.ds_x == nullptr &&
+         (a.relu != kActSwish || (a.Cout & 3) == 0);
+}
+
+hipError_t launch_conv2d_pw(const ConvArgs& a, hipStream_t stream) {
+  const bool sw = a.relu == kActSwish;
+  switch (a.Kp / kKStep) {
+    case 1: return sw ? launch_pw_cfg<1, true>(a, stream) : launch_pw_cfg<1, false>(a, stream);
+    case 2: return sw ? launch_pw_cfg<2, true>(a, stream) : launch_pw_cfg<2, false>(a, stream);
+    case 3: return sw ? launch_pw_cfg<3, true>(a, stream) : launch_pw_cfg<3, false>(a, stream);
+    default: return sw ? launch_pw_cfg<4, true>(a, stream) : launch_pw_cfg<4, false>(a, stream);
+  }
 }
 
 // mb: 1 = 64 x 128 tiles, 2 = 128 x 128 tiles.

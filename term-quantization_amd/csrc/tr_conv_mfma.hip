@@ -479,7 +479,7 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // stride 1, KH*KW >= 2, NHWC out; else the gather default).
 // 9-10 direct (tr_conv_direct.hip: Cp % 64 == 0, NHWC out; 128 x 128 / 64 x 128 tiles).
 // 11 row strip (tr_conv_strip.hip: 3x3/1, 64 -> 64 channels, W <= 56; else the default).
-int conv_mfma_num_configs() { return 11; }
+int conv_mfma_num_configs() { return 12; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
@@ -494,6 +494,10 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   a.ab = ab ? atoi(ab) : 0;
   static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 MB
   if (cfg < 0 && dir && atoi(dir) > 0) cfg = atoi(dir) == 1 ? 9 : 8;
+  // 1x1 convs with K <= 4 K-steps: the persistent pointwise engine (TQ_PW=0: off, A/B)
+  const char* pw = getenv("TQ_PW");  // read per launch: tests switch it
+  if ((cfg < 0 || cfg == 11) && !(pw && atoi(pw) == 0) && conv_pw_eligible(a, out_nhwc))
+    return launch_conv2d_pw(a, stream);
   if (a.relu == kActSwish) {  // the swish epilogue exists on the direct engine only
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
     return launch_conv2d_direct(a, 1, stream);

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 import oracle
 import tq_native
+import tq_ops
 import tr_layer
 
 pytestmark = pytest.mark.gpu
@@ -257,3 +258,52 @@ def _same(ref, got, what):
                          "zero %d, nan %d" % (what, int(bad.sum()), lo, hi, idx[:4].tolist(),
                                               int((g == 0).sum()),
                                               int(torch.isnan(g.float()).sum())))
+
+
+@pytest.mark.parametrize("shape", [
+    # cin, cout, stride, n, h, relu, residual: MobileNet-V2 / EfficientNet 1x1 shapes (expand,
+    # project with a residual, swish), ResNet downsamples (stride 2), partial K / Cout tiles,
+    # a pixel count that is not a multiple of the 128-pixel tile
+    (16, 96, 1, 3, 17, 6, False), (32, 16, 1, 2, 23, 0, False), (96, 24, 1, 2, 14, 0, True),
+    (24, 144, 1, 2, 9, "swish", False), (64, 128, 2, 2, 14, 0, False),
+    (128, 256, 2, 1, 10, 0, False), (160, 960, 1, 1, 7, 6, False), (40, 20, 1, 3, 5, 1, True),
+])
+def test_pointwise_engine_bit_identical(shape, monkeypatch):
+    """The persistent pointwise engine (tr_conv_direct.hip conv2d_tp_pw_kernel: 1x1 convs with
+    <= 3 K-steps, weights staged once per workgroup, next tile's fragments in flight) against
+    the direct engine (TQ_PW=0): the same exact sums and shared epilogue, so outputs and codes
+    are bit-identical."""
+    monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
+    cin, cout, s, n, h, relu, resid = shape
+    torch.manual_seed(cin * 7 + cout)
+    conv = nn.Conv2d(cin, cout, 1, s, 0, bias=False)
+    lay = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 9, 8, 12)
+    assert lay.engine == "mfma"
+    cp = lay.act_channels
+    x = torch.relu(torch.randn(n, cin, h, h, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.zeros((n, h, h, cp), dtype=torch.float16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    ho = (h - 1) // s + 1
+    sc = torch.rand(cout, dtype=torch.float64, device=DEV) * 1e-4
+    sh = torch.randn(cout, dtype=torch.float64, device=DEV) * 0.1
+    res = torch.randn(n, cout, ho, ho, device=DEV).contiguous(
+        memory_format=torch.channels_last) if resid else None
+    cpo = tq_ops.act_channels(cout)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("TQ_PW", mode)
+        o = torch.full((n, cout, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.full((n, ho, ho, cpo), float("nan"), dtype=torch.float16, device=DEV)
+        tq_native.conv2d_termpair_fused(
+            codes, lay.w_codes, cout, 1, 1, (s, s), (0, 0), (1, 1), ho, ho, out=o,
+            ch_scale=sc, ch_shift=sh, residual=res, relu=relu,
+            codes_a=ca if relu not in (0, "swish") else None,
+            quant_a=(0.05, 9, 3) if relu not in (0, "swish") else None, kc_steps=lay.kc_steps)
+        outs.append((o.cpu(), ca.cpu()))
+    (o0, a0), (o1, a1) = outs
+    assert not torch.isnan(o0).any()
+    _same(o0.permute(0, 2, 3, 1), o1.permute(0, 2, 3, 1), "out")
+    if relu not in (0, "swish"):
+        _same(a0.view(torch.int16), a1.view(torch.int16), "codes_a")

@@ -1,0 +1,18 @@
+#!/bin/bash
+# r03e: LSTM fused step kernel (tests + timings + trace)
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; TAG=${1:-r03e}; O=gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_lstm.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -1 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" $O/tests.log | head -20; exit $rc; }
+for v in "TQ_LSTM_SEQ=0" "TQ_LSTM_UPPER=miopen" "TQ_LSTM_SEQ=1"; do
+  env $v timeout -k 10 300 python3 tools/lstm_trace.py --chunks 20 > $O/lstm_$v.log 2>&1 || { tail $O/lstm_$v.log; exit 1; }
+  echo "$v $(tail -1 $O/lstm_$v.log)"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/lstm_kt -o kt -- python3 tools/lstm_trace.py --chunks 10 > $O/lstm_kt.log 2>&1 || { tail $O/lstm_kt.log; exit 1; }
+python3 - <<PY
+import csv
+rows=list(csv.DictReader(open('$O/lstm_kt/kt_kernel_stats.csv')))
+for r in rows[:12]:
+    print("%-80s %6s %9.1f us" % (r['Name'][:80], r['Calls'], float(r['AverageNs'])/1e3))
+PY
