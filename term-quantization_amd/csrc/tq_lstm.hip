@@ -89,14 +89,21 @@ __global__ __launch_bounds__(kStepThreads) void lstm_step_kernel(LstmStepArgs a)
   // dot-product role: gate row r (gate r / nu, unit u0 + r % nu), segment s
   const int r = tid / kStepSeg, s = tid % kStepSeg;
   const bool dot = r < 4 * nu;
-  const int grow = dot ? (r / nu) * H + u0 + (r % nu) : 0;
   const int j0 = s * L;
+  // this workgroup's 4 nu rows of W_hh, staged through LDS with coalesced loads (a lane's
+  // own 1/16 row segment straight from global memory is a 64-way scattered access per
+  // instruction), then into registers
+  float* wrows = part + (int64_t)4 * a.nu * B * kStepSeg;  // [4 nu][H]
+  for (int i = tid; i < 4 * nu * H; i += kStepThreads) {
+    const int rr = i / H, j = i - (i / H) * H;
+    wrows[i] = a.w[(int64_t)((rr / nu) * H + u0 + (rr % nu)) * H + j];
+  }
+  for (int i = tid; i < B * H; i += kStepThreads) hprev[i] = a.h_prev[i];
+  __syncthreads();
   float wreg[kStepLMax];
 #pragma unroll
   for (int i = 0; i < kStepLMax; ++i)
-    wreg[i] = (dot && i < L && j0 + i < H) ? a.w[(int64_t)grow * H + j0 + i] : 0.0f;
-  for (int i = tid; i < B * H; i += kStepThreads) hprev[i] = a.h_prev[i];
-  __syncthreads();
+    wreg[i] = (dot && i < L && j0 + i < H) ? wrows[(int64_t)r * H + j0 + i] : 0.0f;
   if (dot) {
     for (int bb = 0; bb < B; ++bb) {
       const float* hp = hprev + (int64_t)bb * H + j0;
@@ -143,7 +150,8 @@ hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, cons
   a.H = (int)H;
   a.nu = (int)((H + 255) / 256);  // <= 4 for H <= 1024
   const int grid = (int)((H + a.nu - 1) / a.nu);
-  const size_t lds = ((size_t)B * H + (size_t)4 * a.nu * B * kStepSeg) * sizeof(float);
+  const size_t lds =
+      ((size_t)B * H + (size_t)4 * a.nu * B * kStepSeg + (size_t)4 * a.nu * H) * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_step_kernel),

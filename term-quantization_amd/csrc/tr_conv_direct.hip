@@ -442,13 +442,21 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_pw_kernel(ConvArgs a
   };
   auto tile = [&](int64_t nt, const u32x4 (&b)[NKS][4]) __attribute__((always_inline)) {
     const int64_t wn0 = nt * C::BN + wave * 32;
-    float4 res[32 / PXI];  // residuals first: their latency overlaps the MFMAs
+    // residuals first (their latency overlaps the MFMAs), as unconditional loads: a lane
+    // without one reads the zero page (a per-lane branch around each load made the compiler
+    // drain every load in flight, the next tile's fragments included)
+    float4 res[32 / PXI];
+    if (vec && a.residual) {
 #pragma unroll
-    for (int it = 0; it < 32 / PXI; ++it) {
-      const int64_t p = wn0 + it * PXI + lane / C::SL;
-      res[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (vec && a.residual && co < a.Cout && p < a.P)
-        res[it] = *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co);
+      for (int it = 0; it < 32 / PXI; ++it) {
+        const int64_t p = wn0 + it * PXI + lane / C::SL;
+        const bool ok = co < a.Cout && p < a.P;
+        res[it] = *reinterpret_cast<const float4*>(
+            ok ? a.residual + p * a.Cout + co : reinterpret_cast<const float*>(g_zero_page));
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 32 / PXI; ++it) res[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     float16v acc[2];
 #pragma unroll
@@ -500,15 +508,17 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_pw_kernel(ConvArgs a
     __builtin_amdgcn_wave_barrier();
   };
   // pixel tiles g, g + G, ...: the next tile's fragments are in flight during this one
-  u32x4 b0[NKS][4], b1[NKS][4];
-  int64_t nt = g;
-  if (nt < ntn) load_b(nt, b0);
-  for (; nt < ntn; nt += 2 * (int64_t)G) {
-    if (nt + G < ntn) load_b(nt + G, b1);
-    tile(nt, b0);
-    if (nt + G >= ntn) break;
-    if (nt + 2 * (int64_t)G < ntn) load_b(nt + 2 * (int64_t)G, b0);
-    tile(nt + G, b1);
+  // (unconditional loads: past the last tile every lane reads the zero page)
+  u32x4 bcur[NKS][4];
+  load_b(g, bcur);
+  for (int64_t nt = g; nt < ntn; nt += G) {
+    u32x4 bnext[NKS][4];
+    load_b(nt + G, bnext);
+    tile(nt, bcur);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) bcur[ks][s4] = bnext[ks][s4];
   }
 }
 
