@@ -151,8 +151,10 @@ int tq_act_encode_act(const float* x, int64_t n, int64_t c, int64_t h, int64_t w
                 max_code_bits(fmt), bitwidth);
   if (!(sf > 0.0f && sf <= 3.402823466e38f))
     return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: sf must be finite and > 0");
-  if ((uintptr_t)codes % 16 != 0 || (uintptr_t)x % 16 != 0 || (uintptr_t)out % 16 != 0)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "act_encode_act: x, out, codes must be 16-byte aligned");
+  if ((uintptr_t)codes % 16 != 0 || (uintptr_t)x % 16 != 0 || (uintptr_t)out % 16 != 0 ||
+      (uintptr_t)ch_scale % 16 != 0 || (uintptr_t)ch_shift % 16 != 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT,
+                "act_encode_act: x, out, codes, ch_scale, ch_shift must be 16-byte aligned");
   const int kk = num_keep_terms < 0 ? 0 : num_keep_terms;
   return hip_status(tq::launch_act_encode_act(x, ch_scale, ch_shift, gate, act, out, n, c, h,
                                               w, sf, bitwidth, kk,

@@ -445,9 +445,20 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
     for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? x[pix * C + c0 + i] : 0.0f;
   }
   if (ch_scale) {  // eval BatchNorm as a per-channel fp32 affine (a stem's bn before its act)
+    if (vec) {  // 16-byte coefficient loads (4 per lane instead of 16 scalar ones)
+      const float4 s0 = *reinterpret_cast<const float4*>(ch_scale + c0);
+      const float4 s1 = *reinterpret_cast<const float4*>(ch_scale + c0 + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(ch_shift + c0);
+      const float4 h1 = *reinterpret_cast<const float4*>(ch_shift + c0 + 4);
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      v[i] = c0 + i < C ? fmaf(v[i], ch_scale[c0 + i], ch_shift[c0 + i]) : 0.0f;
+      for (int i = 0; i < 8; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        v[i] = c0 + i < C ? fmaf(v[i], ch_scale[c0 + i], ch_shift[c0 + i]) : 0.0f;
+    }
   }
   float o[8];
 #pragma unroll
@@ -467,9 +478,21 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
     for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? gate[img * C + c0 + i] * v[i] : 0.0f;
   }
   uint32_t b[8];
+  if (act_nonneg(act) && !gate && inv_sf > 0.0 && inv_sf <= 1.0e308) {
+    // ReLU / ReLU6: v >= 0 and never NaN -- the epilogues' sign-free fast path (same codes)
+    const int npeel = relu_peels(maxv, k);
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    b[i] = c0 + i < C ? code_bits(tr_value_g1_inv(v[i], inv_sf, maxv, k), fmt) : 0u;
+    for (int h = 0; h < 2; ++h) {
+      int32_t t4[4];
+      tr_values_relu4(v + 4 * h, inv_sf, maxv, npeel, t4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[4 * h + i] = c0 + 4 * h + i < C ? code_bits(t4[i], fmt) : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      b[i] = c0 + i < C ? code_bits(tr_value_g1_inv(v[i], inv_sf, maxv, k), fmt) : 0u;
+  }
   *reinterpret_cast<uint4*>(codes + pix * Cp + c0) =
       make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
 }
