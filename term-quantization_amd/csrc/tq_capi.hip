@@ -699,10 +699,12 @@ int64_t tq_lstm_seq_workspace_bytes(int64_t batch, int64_t hidden) {
 int tq_lstm_seq_f32(const float* gx, const float* w_hh, const float* b_hh, const float* h0,
                     const float* c0, float* out, float* c_out, int64_t steps, int64_t batch,
                     int64_t hidden, void* workspace, int64_t workspace_bytes, void* stream) {
-  if (steps < 0 || batch < 0 || hidden < 0 || hidden > 1024 || batch * hidden > 16384)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: sizes outside hidden <= 1024, batch * "
-                "hidden <= 16384");
+  if (steps < 0 || batch < 0 || hidden < 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: negative size");
   if (steps * batch * hidden == 0) return TQ_OK;
+  if (tq::lstm_seq_workspace_bytes(batch, hidden) < 0)
+    return fail(TQ_ERR_UNSUPPORTED, "lstm_seq: hidden <= 1024 and the batch's hidden state in "
+                "one workgroup's LDS (tq_lstm_seq_workspace_bytes < 0)");
   if (!gx || !w_hh || !h0 || !c0 || !out || !c_out)
     return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq: null pointer");
   if (workspace_bytes < tq::lstm_seq_workspace_bytes(batch, hidden))

@@ -63,8 +63,7 @@ hipError_t launch_lstm_cell(const float* gx, const float* hh, float* c, float* h
 namespace {
 
 constexpr int kStepThreads = 256;
-constexpr int kStepSeg = 16;   // threads per gate row
-constexpr int kStepLMax = 64;  // weights per thread: H <= 1024
+constexpr int kStepSeg = 16;  // threads per gate row
 
 struct LstmStepArgs {
   const float* gx;      // [B][4H] this step's input projection (incl. b_ih)
@@ -77,41 +76,45 @@ struct LstmStepArgs {
   int B, H, nu;
 };
 
+// L = segment length (compile time: every dot-product loop is straight-line code with no
+// per-element guard); rows of h and W are staged zero-padded to HP = 16 L columns.
+template <int L>
 __global__ __launch_bounds__(kStepThreads) void lstm_step_kernel(LstmStepArgs a) {
+  constexpr int HP = kStepSeg * L;
   extern __shared__ float step_lds[];
   const int H = a.H, B = a.B;
-  float* hprev = step_lds;                  // [B][H]
-  float* part = step_lds + (int64_t)B * H;  // [4 nu][B][kStepSeg]
   const int tid = threadIdx.x;
   const int u0 = blockIdx.x * a.nu;
   const int nu = min(a.nu, H - u0);  // units of this workgroup (the last may own fewer)
-  const int L = (H + kStepSeg - 1) / kStepSeg;
+  float* hprev = step_lds;                         // [B][HP]
+  float* wrows = hprev + (int64_t)B * HP;          // [4 nu][HP]
+  float* part = wrows + (int64_t)4 * a.nu * HP;    // [4 nu][B][kStepSeg]
+  // this workgroup's 4 nu rows of W_hh and h_{t-1}, staged with coalesced loads (a lane's own
+  // 1/16 row segment straight from global memory is a scattered access per instruction)
+  for (int rr = 0; rr < 4 * nu; ++rr) {
+    const float* src = a.w + (int64_t)((rr / nu) * H + u0 + (rr % nu)) * H;
+    for (int j = tid; j < HP; j += kStepThreads) wrows[rr * HP + j] = j < H ? src[j] : 0.0f;
+  }
+  for (int bb = 0; bb < B; ++bb)
+    for (int j = tid; j < HP; j += kStepThreads)
+      hprev[bb * HP + j] = j < H ? a.h_prev[(int64_t)bb * H + j] : 0.0f;
+  __syncthreads();
   // dot-product role: gate row r (gate r / nu, unit u0 + r % nu), segment s
   const int r = tid / kStepSeg, s = tid % kStepSeg;
-  const bool dot = r < 4 * nu;
-  const int j0 = s * L;
-  // this workgroup's 4 nu rows of W_hh, staged through LDS with coalesced loads (a lane's
-  // own 1/16 row segment straight from global memory is a 64-way scattered access per
-  // instruction), then into registers
-  float* wrows = part + (int64_t)4 * a.nu * B * kStepSeg;  // [4 nu][H]
-  for (int i = tid; i < 4 * nu * H; i += kStepThreads) {
-    const int rr = i / H, j = i - (i / H) * H;
-    wrows[i] = a.w[(int64_t)((rr / nu) * H + u0 + (rr % nu)) * H + j];
-  }
-  for (int i = tid; i < B * H; i += kStepThreads) hprev[i] = a.h_prev[i];
-  __syncthreads();
-  float wreg[kStepLMax];
+  if (r < 4 * nu) {
+    float wreg[L];
 #pragma unroll
-  for (int i = 0; i < kStepLMax; ++i)
-    wreg[i] = (dot && i < L && j0 + i < H) ? wrows[(int64_t)r * H + j0 + i] : 0.0f;
-  if (dot) {
+    for (int i = 0; i < L; ++i) wreg[i] = wrows[r * HP + s * L + i];
     for (int bb = 0; bb < B; ++bb) {
-      const float* hp = hprev + (int64_t)bb * H + j0;
-      float acc = 0.0f;
+      const float* hp = hprev + bb * HP + s * L;
+      float acc0 = 0.0f, acc1 = 0.0f;  // two chains; fixed order
 #pragma unroll
-      for (int i = 0; i < kStepLMax; ++i)
-        if (i < L && j0 + i < H) acc = fmaf(hp[i], wreg[i], acc);
-      part[((int64_t)r * B + bb) * kStepSeg + s] = acc;
+      for (int i = 0; i + 1 < L; i += 2) {
+        acc0 = fmaf(hp[i], wreg[i], acc0);
+        acc1 = fmaf(hp[i + 1], wreg[i + 1], acc1);
+      }
+      if (L & 1) acc0 = fmaf(hp[L - 1], wreg[L - 1], acc0);
+      part[((int64_t)r * B + bb) * kStepSeg + s] = acc0 + acc1;
     }
   }
   __syncthreads();
@@ -135,9 +138,48 @@ __global__ __launch_bounds__(kStepThreads) void lstm_step_kernel(LstmStepArgs a)
   }
 }
 
+template <int L>
+hipError_t launch_lstm_steps(LstmStepArgs a, const float* gx, const float* h0, const float* c0,
+                             float* out, float* cT, int64_t T, hipStream_t stream) {
+  constexpr int HP = kStepSeg * L;
+  const int64_t B = a.B, H = a.H;
+  const int grid = (int)((H + a.nu - 1) / a.nu);
+  const size_t lds =
+      ((size_t)B * HP + (size_t)4 * a.nu * HP + (size_t)4 * a.nu * B * kStepSeg) * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_step_kernel<L>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  for (int64_t t = 0; t < T; ++t) {
+    a.gx = gx + t * B * 4 * H;
+    a.h_prev = t == 0 ? h0 : out + (t - 1) * B * H;
+    a.c_prev = t == 0 ? c0 : cT;
+    a.h = out + t * B * H;
+    a.c = cT;
+    lstm_step_kernel<L><<<dim3(grid), kStepThreads, lds, stream>>>(a);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
-int64_t lstm_seq_workspace_bytes(int64_t, int64_t) { return 0; }
+// Segment length of the step kernel for hidden size H (the templated L), 0 if H > 1024.
+static int64_t lstm_seg_len(int64_t H) {
+  const int64_t seg = (H + kStepSeg - 1) / kStepSeg;
+  return seg <= 16 ? 16 : seg <= 32 ? 32 : seg <= 41 ? 41 : seg <= 48 ? 48 : seg <= 64 ? 64 : 0;
+}
+
+// 0 (no workspace) when the step kernel's LDS holds the shape, else -1 (unsupported).
+int64_t lstm_seq_workspace_bytes(int64_t B, int64_t H) {
+  const int64_t L = lstm_seg_len(H);
+  if (B < 1 || H < 1 || L == 0) return -1;
+  const int64_t HP = kStepSeg * L, nu = (H + 255) / 256;
+  const int64_t lds = (B * HP + 4 * nu * HP + 4 * nu * B * kStepSeg) * 4;
+  return lds <= 160 * 1024 ? 0 : -1;
+}
 
 hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, const float* h0,
                            const float* c0, float* out, float* cT, int64_t T, int64_t B,
@@ -149,25 +191,14 @@ hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, cons
   a.B = (int)B;
   a.H = (int)H;
   a.nu = (int)((H + 255) / 256);  // <= 4 for H <= 1024
-  const int grid = (int)((H + a.nu - 1) / a.nu);
-  const size_t lds =
-      ((size_t)B * H + (size_t)4 * a.nu * B * kStepSeg + (size_t)4 * a.nu * H) * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_step_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
+  switch (lstm_seg_len(H)) {
+    case 16: return launch_lstm_steps<16>(a, gx, h0, c0, out, cT, T, stream);
+    case 32: return launch_lstm_steps<32>(a, gx, h0, c0, out, cT, T, stream);
+    case 41: return launch_lstm_steps<41>(a, gx, h0, c0, out, cT, T, stream);  // H = 650
+    case 48: return launch_lstm_steps<48>(a, gx, h0, c0, out, cT, T, stream);
+    case 64: return launch_lstm_steps<64>(a, gx, h0, c0, out, cT, T, stream);
+    default: return hipErrorInvalidValue;
   }
-  for (int64_t t = 0; t < T; ++t) {
-    a.gx = gx + t * B * 4 * H;
-    a.h_prev = t == 0 ? h0 : out + (t - 1) * B * H;
-    a.c_prev = t == 0 ? c0 : cT;
-    a.h = out + t * B * H;
-    a.c = cT;
-    lstm_step_kernel<<<dim3(grid), kStepThreads, lds, stream>>>(a);
-  }
-  return hipGetLastError();
 }
 
 }  // namespace tq

@@ -494,9 +494,12 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   a.ab = ab ? atoi(ab) : 0;
   static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 MB
   if (cfg < 0 && dir && atoi(dir) > 0) cfg = atoi(dir) == 1 ? 9 : 8;
-  // 1x1 convs with K <= 4 K-steps: the persistent pointwise engine (TQ_PW=0: off, A/B)
+  // 1x1 convs with K <= 3 K-steps: the persistent pointwise engine on request only (config
+  // 12, or TQ_PW=1): measured slower than the direct engine's one-shot tiles (fused
+  // MobileNet-V2 1x1 convs 92 vs 77 us, EfficientNet-b0 142 vs 108 us: r03g), 2 persistent
+  // workgroups per CU hide less latency than 4 resident one-shot ones
   const char* pw = getenv("TQ_PW");  // read per launch: tests switch it
-  if ((cfg < 0 || cfg == 11) && !(pw && atoi(pw) == 0) && conv_pw_eligible(a, out_nhwc))
+  if ((cfg == 11 || (cfg < 0 && pw && atoi(pw) == 1)) && conv_pw_eligible(a, out_nhwc))
     return launch_conv2d_pw(a, stream);
   if (a.relu == kActSwish) {  // the swish epilogue exists on the direct engine only
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;

@@ -234,6 +234,12 @@ def sync_faults():
 _lstm_ws = {}
 
 
+def lstm_seq_workspace_bytes(batch, hidden):
+    """tq_lstm_seq_workspace_bytes: device bytes the recurrence call needs, < 0 if the shape is
+    outside its domain."""
+    return int(lib().tq_lstm_seq_workspace_bytes(batch, hidden))
+
+
 def lstm_seq(gx, w_hh, b_hh, h0, c0, out, c_out):
     """A whole LSTM layer's recurrence in one persistent launch (tq_lstm_seq_f32): gx
     [T, B, 4H], w_hh [4H, H], b_hh [4H] or None, h0/c0/c_out [B, H], out [T, B, H], contiguous

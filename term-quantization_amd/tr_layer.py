@@ -498,8 +498,8 @@ class TRLSTMLayer(nn.Module):
 
     @staticmethod
     def _seq_kernel(batch, hidden):
-        return (os.environ.get("TQ_LSTM_SEQ", "1") != "0" and hidden <= 1024 and
-                batch * hidden <= 16384)
+        return (os.environ.get("TQ_LSTM_SEQ", "1") != "0" and
+                tq_native.lstm_seq_workspace_bytes(batch, hidden) >= 0)
 
     def forward(self, emb, hidden):
         if self.termpair and not self.input_quant.tracking and emb.is_cuda:

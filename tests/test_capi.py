@@ -227,9 +227,11 @@ def test_lstm_seq_argument_validation():
     buf = torch.zeros(1 << 16, dtype=torch.float32)
     p = buf.data_ptr()
     rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 10, 1100, p, 1 << 20, None)
-    assert rc == 1 and b"hidden <= 1024" in lib.tq_last_error()
+    assert rc == 2 and b"hidden <= 1024" in lib.tq_last_error()
     rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 100, 650, p, 1 << 20, None)
-    assert rc == 1 and b"batch * hidden" in lib.tq_last_error()
+    assert rc == 2 and b"LDS" in lib.tq_last_error()
+    assert tq_native.lstm_seq_workspace_bytes(10, 650) == 0
+    assert tq_native.lstm_seq_workspace_bytes(100, 650) < 0
     need = lib.tq_lstm_seq_workspace_bytes(10, 650)
     assert need == 0
     rc = lib.tq_lstm_seq_f32(p, p, None, p, p, p, p, 35, 10, 650, p, need - 8, None)
