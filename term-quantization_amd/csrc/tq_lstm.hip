@@ -64,6 +64,7 @@ namespace {
 
 constexpr int kStepThreads = 256;
 constexpr int kStepSeg = 16;  // threads per gate row
+constexpr int kStageRows = 16;  // rows per staging batch
 
 struct LstmStepArgs {
   const float* gx;      // [B][4H] this step's input projection (incl. b_ih)
@@ -89,15 +90,50 @@ __global__ __launch_bounds__(kStepThreads) void lstm_step_kernel(LstmStepArgs a)
   float* hprev = step_lds;                         // [B][HP]
   float* wrows = hprev + (int64_t)B * HP;          // [4 nu][HP]
   float* part = wrows + (int64_t)4 * a.nu * HP;    // [4 nu][B][kStepSeg]
-  // this workgroup's 4 nu rows of W_hh and h_{t-1}, staged with coalesced loads (a lane's own
-  // 1/16 row segment straight from global memory is a scattered access per instruction)
-  for (int rr = 0; rr < 4 * nu; ++rr) {
-    const float* src = a.w + (int64_t)((rr / nu) * H + u0 + (rr % nu)) * H;
-    for (int j = tid; j < HP; j += kStepThreads) wrows[rr * HP + j] = j < H ? src[j] : 0.0f;
+  // cell-role operands first (their latency hides behind the staging below)
+  const bool cell = tid < B * nu;
+  const int ct = cell ? tid : 0;  // loads of non-cell threads stay in bounds (unused)
+  const int cb = ct / nu, cu = ct - (ct / nu) * nu;
+  const float* bsrc = a.b ? a.b : a.gx;  // no branch: the bias select happens at use
+  float gpre[4], bpre[4];
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    const int col = gi * H + u0 + cu;
+    gpre[gi] = a.gx[(int64_t)cb * 4 * H + col];
+    bpre[gi] = bsrc[col];
   }
-  for (int bb = 0; bb < B; ++bb)
-    for (int j = tid; j < HP; j += kStepThreads)
-      hprev[bb * HP + j] = j < H ? a.h_prev[(int64_t)bb * H + j] : 0.0f;
+  const float cprev = a.c_prev[(int64_t)cb * H + u0 + cu];
+  // this workgroup's 4 nu rows of W_hh, then the B rows of h_{t-1}, staged zero-padded with
+  // coalesced loads, kStageRows rows per batch: all of a batch's loads are in flight before
+  // its LDS stores (one L2 round trip per batch, not per row)
+  constexpr int JC = (HP + kStepThreads - 1) / kStepThreads;
+  const int nq = 4 * nu + B;
+  for (int q0 = 0; q0 < nq; q0 += kStageRows) {
+    float v[kStageRows][JC];
+#pragma unroll
+    for (int i = 0; i < kStageRows; ++i) {
+      const int q = min(q0 + i, nq - 1);  // clamped: in-bounds loads, no branches
+      const float* src = q < 4 * nu ? a.w + (int64_t)((q / nu) * H + u0 + q % nu) * H
+                                    : a.h_prev + (int64_t)(q - 4 * nu) * H;
+#pragma unroll
+      for (int jj = 0; jj < JC; ++jj) {
+        const int j = tid + jj * kStepThreads;
+        const float x = src[min(j, H - 1)];
+        v[i][jj] = j < H ? x : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kStageRows; ++i) {
+      const int q = q0 + i;
+      if (q >= nq) break;
+      float* dst = q < 4 * nu ? wrows + q * HP : hprev + (q - 4 * nu) * HP;
+#pragma unroll
+      for (int jj = 0; jj < JC; ++jj) {
+        const int j = tid + jj * kStepThreads;
+        if (j < HP) dst[j] = v[i][jj];
+      }
+    }
+  }
   __syncthreads();
   // dot-product role: gate row r (gate r / nu, unit u0 + r % nu), segment s
   const int r = tid / kStepSeg, s = tid % kStepSeg;
@@ -118,8 +154,7 @@ __global__ __launch_bounds__(kStepThreads) void lstm_step_kernel(LstmStepArgs a)
     }
   }
   __syncthreads();
-  if (tid < B * nu) {  // cell role: (batch row cb, unit u0 + cu)
-    const int cb = tid / nu, cu = tid - (tid / nu) * nu;
+  if (cell) {  // cell role: (batch row cb, unit u0 + cu)
     float gate[4];
 #pragma unroll
     for (int gi = 0; gi < 4; ++gi) {
@@ -127,12 +162,10 @@ __global__ __launch_bounds__(kStepThreads) void lstm_step_kernel(LstmStepArgs a)
       float sum = 0.0f;
 #pragma unroll
       for (int k = 0; k < kStepSeg; ++k) sum += pp[k];
-      const int col = gi * H + u0 + cu;
-      const float bias = a.b ? a.b[col] : 0.0f;
-      gate[gi] = a.gx[(int64_t)cb * 4 * H + col] + (sum + bias);
+      gate[gi] = gpre[gi] + (sum + (a.b ? bpre[gi] : 0.0f));
     }
     const int64_t o = (int64_t)cb * H + u0 + cu;
-    const float c = sigmoid_f(gate[1]) * a.c_prev[o] + sigmoid_f(gate[0]) * tanhf(gate[2]);
+    const float c = sigmoid_f(gate[1]) * cprev + sigmoid_f(gate[0]) * tanhf(gate[2]);
     a.c[o] = c;
     a.h[o] = sigmoid_f(gate[3]) * tanhf(c);
   }

@@ -31,6 +31,10 @@
 #include "tq_launch.h"
 #include "tq_mfma.h"
 
+#ifndef TQ_ABLATE
+#define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
+#endif
+
 namespace tq {
 
 namespace {
@@ -133,7 +137,11 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     }
   }
 
+#if TQ_ABLATE == 6
+  int nsteps = 0;  // timing only: setup + epilogue
+#else
   int nsteps = a.Kp / kKStep;  // = KH * KW * Cp / 64 (Cp % 64 == 0)
+#endif
   // position of the next K-step to issue, advanced incrementally (no divisions in the loop)
   int i_st = 0, i_tap = 0, i_cb = 0, i_ks = 0;
   int64_t i_toff = 0;  // ((kr * dh) * W + ks * dw) * Cp + cb
@@ -145,6 +153,11 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
 
   // Issue K-step i_st: A-DMA into `slot`, B fragments into b (lane: codes [16s + 8hh, +8)).
   auto issue = [&](int slot, u32x4 (&b)[4]) {
+#if TQ_ABLATE == 3  // timing only: no A DMA, no B loads (fragments from the zero page)
+    (void)slot;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) b[s] = (u32x4)(uint32_t)(i_st + s);
+#else
 #pragma unroll
     for (int i = 0; i < C::AI; ++i)
       glds16(arow[i] + (int64_t)i_st * kKStep,
@@ -158,6 +171,7 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       b[s] = *reinterpret_cast<const u32x4*>((16 * s < cleft ? src : zero) + 16 * s);
+#endif
     ++i_st;
     i_cb += kKStep;
     i_toff += kKStep;
@@ -205,7 +219,11 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
 #pragma unroll
       for (int bm = 0; bm < NBM; ++bm) {
         const half8 af = __builtin_bit_cast(half8, img[swz(32 * bm + r32, c)]);
+#if TQ_ABLATE == 2  // timing only: no MFMA (fragments kept live)
+        asm volatile("" ::"v"(af), "v"(bf));
+#else
         accf[bm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, accf[bm], 0, 0, 0);
+#endif
       }
     }
     if (FLUSH && ++since_flush == kc_steps) {
@@ -342,6 +360,10 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     if (p >= a.P) continue;
     const u32x4 v = t[px * C::SL + (slot ^ (px & 15))];
     const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+#if TQ_ABLATE == 7  // timing only: no epilogue stores (sums kept live)
+    if (acc4[0] == 0x7fffffff && a.out) a.out[p] = res[it].x + (float)(sc[0] + sh[0]);
+    continue;
+#endif
     if (vec)
       emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
