@@ -90,6 +90,7 @@ class KernelTimer(object):
         self.events = {}
         self.work = {}
         self.nbytes = {}
+        self.per_launch = {}  # name -> [(work, bytes)] in launch order
         # time base on the launching stream: every kernel event (on any chunk stream, each
         # of which first waits on this stream) comes after it on the device timeline
         self.base = torch.cuda.Event(enable_timing=True)
@@ -103,6 +104,7 @@ class KernelTimer(object):
         r = fn()
         b.record(s)
         self.events.setdefault(name, []).append((a, b))
+        self.per_launch.setdefault(name, []).append((work, nbytes))
         self.work[name] = self.work.get(name, 0) + work
         self.nbytes[name] = self.nbytes.get(name, 0) + nbytes
         return r
@@ -126,7 +128,8 @@ class KernelTimer(object):
             if cur_e is not None:
                 busy += cur_e - cur_s
             out[name] = {"launches": len(evs), "seconds": t, "busy": busy * 1e-3,
-                         "work": self.work[name], "bytes": self.nbytes[name]}
+                         "work": self.work[name], "bytes": self.nbytes[name],
+                         "per_launch": self.per_launch[name]}
         return out
 
 
@@ -471,6 +474,18 @@ def main():
             # the north star's HBM roofline of the whole path: 15,026,432
             # algorithmic bytes per image (fp32 TR-layer inputs + outputs + weights/256) at
             # the measured images/s against the 8 TB/s HBM peak
+            # per-launch roofline: each launch's bound is the larger of its MFMA time
+            # (2 * MACs / fp16 peak) and its HBM time (algorithmic bytes / 8 TB/s); the
+            # sum of those floors over the convs' summed launch durations (layer-1/2 convs
+            # and every fp32-residual conv2 sit on the HBM side of the ridge)
+            "per_launch_bound_frac": (sum(max(2 * w / (MFMA_F16_PEAK_TFLOPS * 1e12),
+                                               nb / (HBM_PEAK_GBS * 1e9))
+                                           for w, nb in conv["per_launch"]) / conv["seconds"]
+                                      if mfma else None),
+            "per_launch_hbm_bound_launches": (sum(
+                1 for w, nb in conv["per_launch"]
+                if nb / (HBM_PEAK_GBS * 1e9) > 2 * w / (MFMA_F16_PEAK_TFLOPS * 1e12))
+                if mfma else None),
             "hbm_bytes_per_image": HBM_BYTES_PER_IMAGE,
             "hbm_frac": HBM_BYTES_PER_IMAGE * ips / (HBM_PEAK_GBS * 1e9),
         })
