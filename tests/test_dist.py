@@ -93,6 +93,10 @@ def _grid_worker(rank, world, port, out_dir, out):
     torch.set_num_threads(max(1, 8 // world))
     import evaluate_cnn
     import evaluate_group_size
+    # a corner subset of the 25-point grid keeps the CPU suite short (the whole grid runs at
+    # world 1 under -m gpu, tests/test_gpu_grid.py); the sharding is what is checked here
+    evaluate_group_size.GROUP_SIZES = [1, 32]
+    evaluate_group_size.AVG_TERM_SETTINGS = [1.0, 3.0]
     seen = []
     validate = evaluate_cnn.util.validate
 
@@ -111,7 +115,7 @@ def test_evaluate_group_size_world2_equals_world1(tmp_path):
     """BASELINE configs[4] through the code torchrun launches: evaluate_group_size.py --synthetic
     on the CPU (gloo) at world 1 and world 2.  Rank-strided batches, histograms summed over
     ranks and integer counters make the results JSON -- and every (loss, top-1) pass of the
-    25 settings -- identical at both world sizes; the written file equals the returned dict."""
+    grid-corner settings -- identical at both world sizes; the written file equals the returned dict."""
     import json
     mgr = mp.Manager()
     runs = {}
@@ -124,12 +128,13 @@ def test_evaluate_group_size_world2_equals_world1(tmp_path):
         assert written == runs[world][0][0]
     r1, seen1 = runs[1][0]
     r2, seen2 = runs[2][0]
-    assert r1 == r2 and seen1 == seen2 and len(seen1) == 50
+    assert r1 == r2 and seen1 == seen2 and len(seen1) == 8
     assert runs[2][1] == runs[2][0]  # both ranks return the global figures
     pub = json.load(open(os.path.join(HERE, "golden", "published_results.json")))[
         "resnet18-group-size-results.json"]
-    for g in ("1", "2", "8", "16", "32"):  # the published term-pair MAC counts per setting
-        assert r1[g]["tmacs"] == pub[g]["tmacs"] and r1[g]["avg_terms"] == pub[g]["avg_terms"]
+    for g in ("1", "32"):  # the published term-pair MAC counts per setting (avg 1.0 and 3.0)
+        assert r1[g]["tmacs"] == [pub[g]["tmacs"][i] for i in (0, 4)]
+        assert r1[g]["avg_terms"] == [pub[g]["avg_terms"][i] for i in (0, 4)]
 
 
 def test_sharded_loader_covers_a_map_style_dataset_once():
