@@ -181,7 +181,13 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
     tile_max[0] = 0u;
     tile_max[1] = 0u;
   }
-  if (blockIdx.x < tiles) prefetch(blockIdx.x);
+  // Each workgroup walks a contiguous run of tiles (top to bottom through its images): the
+  // 2 TP + 4 s2d rows of a tile overlap the previous tile's by 4, and those halo rows were
+  // fetched by this workgroup one tile earlier, so they come from L2 instead of HBM (a
+  // strided tile order put vertically adjacent tiles on different XCDs: 1.47x input FETCH).
+  const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
+  const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
+  if (t_begin < t_end) prefetch(t_begin);
   __syncthreads();
 
   // fp16 operands need a range: each tile's inputs are scaled by 2^kx so that max |x| <
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   // (it & 1) is written before barrier A and read between A and B, the other slot is
   // cleared between A and B for the next tile.
   int it = 0;
-  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, ++it) {
+  for (int tile = t_begin; tile < t_end; ++tile, ++it) {
     const int n = tile / tpi;
     const int py0 = (tile - n * tpi) * TP;
     {
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
     commit(kx);
     if (tid == 0) tile_max[(it + 1) & 1] = 0u;
     __syncthreads();  // B
-    if (tile + (int)gridDim.x < tiles) prefetch(tile + gridDim.x);
+    if (tile + 1 < t_end) prefetch(tile + 1);
 
     for (int b = wave; b < nb; b += kStemThreads / 64) {
       const int c0 = 14 * b - 1;  // first conv column of the strip

@@ -64,12 +64,16 @@ template <int MB, bool FLUSH, bool DS, bool SWISH>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
   constexpr int NBM = 2 * MB;  // 32-row MFMA blocks per wave
-  __shared__ __attribute__((aligned(16))) u32x4 lds[C::LDS];
+  // the A ring + epilogue tile in DYNAMIC LDS (then the code tables): with a static array the
+  // compiler drains every load in flight (s_waitcnt vmcnt(0)) before each ring read, as the
+  // read may alias the LDS-DMA just issued -- the next K-steps' prefetch included
+  extern __shared__ __attribute__((aligned(16))) u32x4 dyn_lds[];
+  u32x4* lds = dyn_lds;
   __shared__ double coef[C::BM][2];  // epilogue (scale, shift) of the tile's channels
   __shared__ double coef2[DS ? C::BM : 1][2];  // the fused downsample's (scale, shift)
-  extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lut[];  // epilogue code tables
   uint16_t *lut_a, *lut_b;
-  conv_luts(a, dyn_lut, lut_a, lut_b);  // read only after the epilogue's barrier
+  conv_luts(a, reinterpret_cast<uint16_t*>(dyn_lds + C::LDS), lut_a, lut_b);  // read after
+                                                                              // the epilogue's barrier
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = (a.Cout + C::BM - 1) / C::BM;
@@ -562,8 +566,17 @@ template <int MB, bool FLUSH, bool DS, bool SWISH = false>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   using C = DirCfg<MB>;
   const int64_t tiles = ((a.P + C::BN - 1) / C::BN) * ((a.Cout + C::BM - 1) / C::BM);
+  static bool attr_set = false;  // the MB = 2 ring + code tables pass the 64 KB default
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH>),
+        hipFuncAttributeMaxDynamicSharedMemorySize,
+        160 * 1024 - (C::BM + (DS ? C::BM : 1)) * 16);  // minus the static coef arrays
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
   conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH>
-      <<<dim3((unsigned)tiles), kDirThreads, (size_t)conv_lut_bytes(a), stream>>>(a);
+      <<<dim3((unsigned)tiles), kDirThreads, (size_t)(C::LDS * 16 + conv_lut_bytes(a)), stream>>>(a);
   return hipGetLastError();
 }
 

@@ -29,6 +29,9 @@
 #ifndef TQ_ABLATE
 #define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
 #endif
+#ifndef TQ_PATCH_SCHED
+#define TQ_PATCH_SCHED 1  // 0: the round-2 schedule (timing variants only, tools/variant.sh)
+#endif
 
 namespace tq {
 
@@ -74,7 +77,8 @@ __host__ __device__ inline PatchRows patch_rows(const ConvArgs& a, int64_t n0) {
 // Slab and counter accesses are agent-scope atomics (sc1 stores/loads that bypass the
 // non-coherent per-XCD L2), ordered by vmcnt(0) before the counter RMW.
 template <int MB, int NR, bool SK>
-__global__ __launch_bounds__(kPatchThreads, MB == 1 ? 4 : 2) void conv2d_tp_patch_kernel(
+__global__ __launch_bounds__(kPatchThreads, TQ_PATCH_SCHED ? (MB == 1 ? 2 : 1) : (MB == 1 ? 4 : 2))
+void conv2d_tp_patch_kernel(
     ConvArgs a) {
   constexpr int BM = 64 * MB;                 // 2 waves x 32*MB Cout rows
   constexpr int AI = MB;                      // weight wave-instructions per wave and step
@@ -289,6 +293,16 @@ __global__ __launch_bounds__(kPatchThreads, MB == 1 ? 4 : 2) void conv2d_tp_patc
           for (int bn = 0; bn < 2; ++bn)
             acc.f[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[k][bm], bf[k][bn],
                                                                    acc.f[bm][bn], 0, 0, 0);
+#if TQ_ABLATE == 0 && TQ_PATCH_SCHED
+      // every fragment read of the step is issued before its first MFMA (the scheduler
+      // otherwise recycles four fragment registers: read 4, wait, 4 MFMAs, ...)
+      // (three K-substeps' reads, then the first substep's MFMAs under the last reads: the
+      // 4-bit lgkmcnt counts at most 15 reads in flight)
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * (MB + 2), 0);  // DS reads, k = 0..2
+      __builtin_amdgcn_sched_group_barrier(0x008, MB * 2, 0);        // MFMAs, k = 0
+      __builtin_amdgcn_sched_group_barrier(0x100, MB + 2, 0);        // DS reads, k = 3
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * MB * 2, 0);    // MFMAs, k = 1..3
+#endif
 #endif
       if (++since_flush == kc_steps || (flushing && t + 1 == ntap)) {
         acc_flush(acc);

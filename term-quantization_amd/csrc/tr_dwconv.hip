@@ -27,21 +27,33 @@ __device__ __forceinline__ int sext24(int v) { return (v << 8) >> 8; }
 // Epilogue of output pixel p (image img, in-image index rem), channels c0 .. c0 + CPL - 1,
 // from the exact int32 sums: one fp64 -> fp32 rounding, activation, fp32 store and/or next
 // codes.  CPL = 4 or 8 channels per lane.
+// Epilogue coefficients of channels c0 .. c0 + CPL - 1: y = fold_acc(acc, sc, sh) (pad
+// channels: sc = sh = 0, so y = 0).
 template <int CPL>
-__device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut, int64_t p,
-                                        int64_t img, int rem, int c0, const int acc[CPL]) {
-  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
-  float y[CPL];
+__device__ __forceinline__ void dw_coef(const DwConvArgs& a, int c0, coef_t sc[CPL],
+                                        coef_t sh[CPL]) {
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = c0 + i;
-    if (a.ch_scale) {  // folded BN (pad channels: 0)
-      y[i] = c < a.C ? fold_acc(acc[i], (coef_t)a.ch_scale[c], (coef_t)a.ch_shift[c]) : 0.0f;
+    if (a.ch_scale) {  // folded BN
+      sc[i] = c < a.C ? (coef_t)a.ch_scale[c] : (coef_t)0;
+      sh[i] = c < a.C ? (coef_t)a.ch_shift[c] : (coef_t)0;
     } else {
-      const double sh = (a.bias && c < a.C) ? (double)a.bias[c] : 0.0;
-      y[i] = fold_acc(acc[i], (coef_t)a.scale, (coef_t)sh);
+      sc[i] = c < a.C ? (coef_t)a.scale : (coef_t)0;
+      sh[i] = (a.bias && c < a.C) ? (coef_t)(double)a.bias[c] : (coef_t)0;
     }
   }
+}
+
+template <int CPL>
+__device__ __forceinline__ void dw_emit_coef(const DwConvArgs& a, const uint16_t* lut,
+                                             int64_t p, int64_t img, int rem, int c0,
+                                             const int acc[CPL], const coef_t sc[CPL],
+                                             const coef_t sh[CPL]) {
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  float y[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) y[i] = fold_acc(acc[i], sc[i], sh[i]);
   const bool full = (a.C % CPL) == 0;
   auto store_nhwc = [&](const float (&v)[CPL]) {
     float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
@@ -93,6 +105,14 @@ __device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut
     for (int i = 0; i < CPL; ++i)
       if (c0 + i < a.C) a.out[(img * a.C + c0 + i) * HoWo + rem] = y[i];
   }
+}
+
+template <int CPL>
+__device__ __forceinline__ void dw_emit(const DwConvArgs& a, const uint16_t* lut, int64_t p,
+                                        int64_t img, int rem, int c0, const int acc[CPL]) {
+  coef_t sc[CPL], sh[CPL];
+  dw_coef<CPL>(a, c0, sc, sh);
+  dw_emit_coef<CPL>(a, lut, p, img, rem, c0, acc, sc, sh);
 }
 
 __device__ __forceinline__ void dw_emit8(const DwConvArgs& a, const uint16_t* lut, int64_t p,
@@ -305,6 +325,115 @@ __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
   }
 }
 
+// Streaming 3x3 depthwise kernel (dilation 1, stride S = 1 or 2).  A lane owns CPL channels of
+// one output column over a segment of output rows, walked in blocks of R rows: the block's
+// NIN = (R - 1) S + 3 input rows are in registers (three column taps each), the NEXT block's
+// R S new input rows are loaded before the block's MACs and epilogue run, and the block's last
+// 3 - S rows are kept for the next one.  So every input row is loaded once per lane (the
+// sliding-window kernel reloads the (3 - S)-row halo of every block), a lane has a block of
+// loads in flight for its whole segment instead of one load-then-compute shot, and the
+// weights and epilogue coefficients are loaded once per segment.  Same exact int32 sums and
+// epilogue as the other depthwise kernels (bit-identical outputs).
+template <int S, int R, int CPL>
+__global__ __launch_bounds__(256) void dwconv3_stream_kernel(DwConvArgs a, int seg) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
+  if (a.lut_c) {
+    lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
+    __syncthreads();
+  }
+  constexpr int NIN = (R - 1) * S + 3;  // input rows of a block
+  constexpr int NEW = R * S;            // rows the next block adds
+  constexpr int KEEP = NIN - NEW;       // rows shared with the next block (3 - S)
+  typedef int v4i __attribute__((ext_vector_type(CPL / 2)));  // CPL int16 codes
+  const int chunks = a.Cp / CPL;
+  const int nseg = (a.Ho + seg - 1) / seg;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t lanes = (int64_t)a.N * nseg * a.Wo * chunks;
+  if (t >= lanes) return;
+  int64_t q = t / chunks;
+  const int c0 = (int)(t - q * chunks) * CPL;
+  const int ow = (int)(q % a.Wo);
+  q /= a.Wo;
+  const int sg = (int)(q % nseg);
+  const int64_t img = q / nseg;
+  const int oh_begin = sg * seg;
+  const int oh_end = oh_begin + seg < a.Ho ? oh_begin + seg : a.Ho;
+  const int iw0 = ow * S - a.pw;
+  int w[9][CPL];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int32_t* wt = a.w + (int64_t)k * a.Cp + c0;
+#pragma unroll
+    for (int i = 0; i < CPL; i += 4) {
+      const int4 wv = *reinterpret_cast<const int4*>(wt + i);
+      w[k][i] = sext24(wv.x);
+      w[k][i + 1] = sext24(wv.y);
+      w[k][i + 2] = sext24(wv.z);
+      w[k][i + 3] = sext24(wv.w);
+    }
+  }
+  coef_t sc[CPL], sh[CPL];
+  dw_coef<CPL>(a, c0, sc, sh);
+  bool cok[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) cok[ks] = iw0 + ks >= 0 && iw0 + ks < a.W;
+  const int16_t* xb = a.x + (int64_t)img * a.H * a.W * a.Cp + c0;
+  const v4i* zero = reinterpret_cast<const v4i*>(&g_dw_zero);
+  // unconditional loads: rows outside the image (or wanted == false) read the zero block
+  auto load_row = [&](int ih, bool wanted, v4i (&dst)[3]) {
+    const bool rok = wanted && ih >= 0 && ih < a.H;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const bool ok = rok && cok[ks];
+      dst[ks] = *(ok ? reinterpret_cast<const v4i*>(xb + ((int64_t)ih * a.W + iw0 + ks) * a.Cp)
+                     : zero);
+    }
+  };
+  const uint16_t* l = a.lut_c ? lut : nullptr;
+  int ih0 = oh_begin * S - a.ph;  // first tap row of the block's first output row
+  v4i cur[NIN][3];
+#pragma unroll
+  for (int k = 0; k < NIN; ++k) load_row(ih0 + k, true, cur[k]);
+  for (int oh0 = oh_begin; oh0 < oh_end; oh0 += R) {
+    v4i nxt[NEW][3];  // the next block's new rows, in flight during this block
+    const bool more = oh0 + R < oh_end;
+#pragma unroll
+    for (int k = 0; k < NEW; ++k) load_row(ih0 + NIN + k, more, nxt[k]);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      int acc[CPL];
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) acc[i] = 0;
+#pragma unroll
+      for (int kr = 0; kr < 3; ++kr)
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          const v4i xv = cur[j * S + kr][ks];
+#pragma unroll
+          for (int i = 0; i < CPL / 2; ++i) {
+            const int lo = (int)(short)(xv[i] & 0xFFFF);
+            const int hi = xv[i] >> 16;
+            acc[2 * i] += lo * w[kr * 3 + ks][2 * i];
+            acc[2 * i + 1] += hi * w[kr * 3 + ks][2 * i + 1];
+          }
+        }
+      const int oh = oh0 + j;
+      if (oh < oh_end)
+        dw_emit_coef<CPL>(a, l, (img * a.Ho + oh) * a.Wo + ow, img, oh * a.Wo + ow, c0, acc,
+                          sc, sh);
+    }
+#pragma unroll
+    for (int k = 0; k < KEEP; ++k)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) cur[k][ks] = cur[NEW + k][ks];
+#pragma unroll
+    for (int k = 0; k < NEW; ++k)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) cur[KEEP + k][ks] = nxt[k][ks];
+    ih0 += NEW;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
@@ -315,6 +444,34 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   static const char* rows_env = getenv("TQ_DW_ROWS");
   const char* slide_env = getenv("TQ_DW_SLIDE");  // read per launch: tests switch it
   const int slide = slide_env ? atoi(slide_env) : 4;
+  // the streaming kernel (default for 3x3 stride 1/2): TQ_DW_STREAM=0 falls back to the
+  // sliding-window / row-blocked kernels (tests and A/B), =6 six rows per block at stride 1
+  const char* stream_env = getenv("TQ_DW_STREAM");
+  const int stream_mode = stream_env ? atoi(stream_env) : 1;
+  if (stream_mode && a.KH == 3 && a.KW == 3 && a.dh == 1 && a.dw == 1 && a.sh == a.sw &&
+      (a.sh == 1 || a.sh == 2) && a.Cp % 4 == 0) {
+    const int S = a.sh;
+    const int R = S == 1 ? (stream_mode == 6 ? 6 : 8) : 4;
+    // segments: enough lanes for about two rounds of 2 waves per SIMD, each lane walking
+    // as many R-row blocks as that leaves (one segment = a whole image column if it fits)
+    const int64_t base = (int64_t)a.N * a.Wo * (a.Cp / 4);
+    const int64_t want = (int64_t)device_cus() * 4 * 2 * 64 * 2;
+    const int nblk = (a.Ho + R - 1) / R;
+    int64_t nseg = (want + base - 1) / base;
+    if (nseg < 1) nseg = 1;
+    if (nseg > nblk) nseg = nblk;
+    int bps = (int)((nblk + nseg - 1) / nseg);  // blocks per segment
+    const char* seg_env = getenv("TQ_DW_SEG");   // tests: force multi-block segments
+    if (seg_env && atoi(seg_env) > 0) bps = atoi(seg_env);
+    const int seg = bps * R;
+    const int64_t lanes = base * ((a.Ho + seg - 1) / seg);
+    const dim3 grid((unsigned)((lanes + 255) / 256));
+    const size_t lds = (size_t)a.lut_c * 2;
+    if (S == 2) dwconv3_stream_kernel<2, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
+    else if (R == 6) dwconv3_stream_kernel<1, 6, 4><<<grid, 256, lds, stream>>>(a, seg);
+    else dwconv3_stream_kernel<1, 8, 4><<<grid, 256, lds, stream>>>(a, seg);
+    return hipGetLastError();
+  }
   if (slide && !(rows_env && atoi(rows_env) == 0) && a.KH == 3 && a.KW == 3 && a.dh == 1 &&
       a.dw == 1 && a.sh == a.sw && (a.sh == 1 || a.sh == 2) && a.Cp % slide == 0) {
     // rows per lane: 8 at stride 1 (10 input rows in flight), 4 at stride 2 (9 rows)

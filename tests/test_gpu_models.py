@@ -184,15 +184,17 @@ def test_depthwise_models_layers_match_reference_composition(arch):
     # c, hw, stride, pad (top, left), ho/wo: plain 3x3 s1 p1, s2 p1 (odd input), MobileNet-V2
     # shapes, static-same s2 (pad 0 top/left, EfficientNet), H % 8 != 0, Cp with pad channels
     (32, 14, 1, (1, 1)), (96, 15, 2, (1, 1)), (144, 28, 2, (1, 1)), (40, 13, 1, (1, 1)),
-    (24, 16, 2, (0, 0)), (20, 9, 1, (1, 1)), (960, 7, 1, (1, 1)),
+    (24, 16, 2, (0, 0)), (20, 9, 1, (1, 1)), (960, 7, 1, (1, 1)), (32, 57, 1, (1, 1)),
+    (16, 61, 2, (0, 0)),
 ])
 @pytest.mark.parametrize("relu", [6, "swish"])
 def test_dw_sliding_window_kernel_bit_identical(cfg, relu, monkeypatch):
-    """The sliding-window 3x3 depthwise kernel (tr_dwconv.hip dwconv3_slide_kernel, 4 or 8
-    channels per lane, weights in registers, tap rows streamed once) against the row-blocked
-    kernel (TQ_DW_SLIDE=0): the same exact int32 sums and epilogue, so the fp32 outputs and the
-    next layer's codes are bit-identical, including partial row blocks, odd sizes, stride 2 and
-    asymmetric (static-same) padding."""
+    """The streaming 3x3 depthwise kernel (tr_dwconv.hip dwconv3_stream_kernel: R-row blocks,
+    the next block's rows in flight, one- and multi-block segments) and the sliding-window
+    kernel (dwconv3_slide_kernel, 4 or 8 channels per lane) against the row-blocked kernel
+    (TQ_DW_SLIDE=0): the same exact int32 sums and epilogue, so the fp32 outputs and the next
+    layer's codes are bit-identical, including partial row blocks and segments, odd sizes,
+    stride 2 and asymmetric (static-same) padding."""
     import tq_native
     c, hw, s, (pt, pl) = cfg
     torch.manual_seed(c + hw)
@@ -207,8 +209,12 @@ def test_dw_sliding_window_kernel_bit_identical(cfg, relu, monkeypatch):
     sc = torch.rand(c, dtype=torch.float64, device=DEV) * 1e-5
     sh = torch.randn(c, dtype=torch.float64, device=DEV) * 0.1
     outs = []
-    for mode in ("0", "4", "8"):
+    # (sliding-window mode, streaming mode, blocks per streaming segment)
+    for mode, stream, seg in (("0", "0", "0"), ("4", "0", "0"), ("8", "0", "0"),
+                              ("4", "1", "0"), ("4", "1", "3"), ("4", "6", "2")):
         monkeypatch.setenv("TQ_DW_SLIDE", mode)
+        monkeypatch.setenv("TQ_DW_STREAM", stream)
+        monkeypatch.setenv("TQ_DW_SEG", seg)
         o = torch.full((3, c, ho, ho), float("nan"), device=DEV).contiguous(
             memory_format=torch.channels_last)
         nc = torch.full((3, ho, ho, cp), -1, dtype=torch.int16, device=DEV)
