@@ -35,7 +35,18 @@
 #define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
 #endif
 
+#ifndef TQ_PHASE_TRACE
+#define TQ_PHASE_TRACE 0  // timing-only builds (tools/variant.sh): per-workgroup phase stamps
+#endif
+
 namespace tq {
+
+#if TQ_PHASE_TRACE
+// [workgroup][start, main loop done, epilogue done, hw id | xcc id << 32] (s_memrealtime ticks,
+// 100 MHz), first kTraceMax workgroups of the last traced launch; read by tq_phase_trace_read
+constexpr int kTraceMax = 1 << 16;
+__device__ unsigned long long g_phase_trace[kTraceMax * 4];
+#endif
 
 namespace {
 
@@ -75,6 +86,9 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   conv_luts(a, reinterpret_cast<uint16_t*>(dyn_lds + C::LDS), lut_a, lut_b);  // read after
                                                                               // the epilogue's barrier
 
+#if TQ_PHASE_TRACE
+  const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = (a.Cout + C::BM - 1) / C::BM;
   const int m0 = (tile % mt) * C::BM;
@@ -260,6 +274,9 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   };
   run();
   if (FLUSH) flush();
+#if TQ_PHASE_TRACE
+  const unsigned long long tr_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (DS) {
     // the main conv's exact sums park in acci; the downsample accumulates from zero
 #pragma unroll
@@ -349,7 +366,11 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     __builtin_amdgcn_wave_barrier();
   }
   put_tile(false);
+#if TQ_PHASE_TRACE
+  if (co < a.Cout) {
+#else
   if (co >= a.Cout) return;
+#endif
   coef_t sc[4], sh[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -373,6 +394,21 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     else
       emit4_nhwc(a, p, co, acc4, sc, sh, false, lut_a, lut_b);
   }
+#if TQ_PHASE_TRACE
+  }
+  // wave 0's stamp once its epilogue stores are issued (not completed: waiting for them
+  // would hold the workgroup's slot longer than the product kernel does)
+  if (threadIdx.x == 0 && blockIdx.x < kTraceMax) {
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+    unsigned long long* r = g_phase_trace + (int64_t)blockIdx.x * 4;
+    r[0] = tr_t0;
+    r[1] = tr_t1;
+    r[2] = t2;
+    r[3] = hw | ((unsigned long long)xcc << 32);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -630,5 +666,13 @@ hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream) {
   if (mb == 2) return launch_direct_mb<2, false>(a, stream);
   return launch_direct_mb<1, false>(a, stream);
 }
+
+#if TQ_PHASE_TRACE
+extern "C" int tq_phase_trace_read(void* dst, int64_t n_wg) {
+  if (n_wg > kTraceMax) n_wg = kTraceMax;
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_phase_trace), (size_t)n_wg * 32, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // namespace tq
