@@ -65,6 +65,23 @@ __device__ __forceinline__ void glds16(const void* src, u32x4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
 }
 
+// The same LDS-DMA issued as inline asm, invisible to the compiler's wait-count pass.  With
+// the builtin, any LDS-DMA in flight makes that pass wait for vmcnt(0) before the first use
+// of ANY vector-register load (it cannot order the two kinds of vmcnt event), which drains
+// a kernel's register prefetch (checked on a two-load test kernel: vmcnt(0) with a DMA in
+// flight, vmcnt(2) without).  Safe for the compiler's own waits: an untracked DMA only makes
+// them wait longer (vmcnt retires in order).  The caller retires the DMA itself (counted
+// TQ_WAIT_VM + barrier) and must keep LDS reads of the slot behind a compiler barrier
+// ("memory" clobber: this asm is one).
+__device__ __forceinline__ void glds16_asm(const void* src, u32x4* lds_wave_base) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(la)
+               : "memory", "m0");
+}
+
 // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 |
 // vmcnt[5:4] << 14), other counters untouched.
 #define TQ_WAIT_VM(n) \

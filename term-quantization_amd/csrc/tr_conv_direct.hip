@@ -35,6 +35,9 @@
 #define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
 #endif
 
+#ifndef TQ_DIR_ASM_DMA
+#define TQ_DIR_ASM_DMA 1  // 0: the weight DMA through the builtin (timing variants only)
+#endif
 #ifndef TQ_PHASE_TRACE
 #define TQ_PHASE_TRACE 0  // timing-only builds (tools/variant.sh): per-workgroup phase stamps
 #endif
@@ -177,9 +180,15 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     for (int s = 0; s < 4; ++s) b[s] = (u32x4)(uint32_t)(i_st + s);
 #else
 #pragma unroll
-    for (int i = 0; i < C::AI; ++i)
+    for (int i = 0; i < C::AI; ++i) {
+#if TQ_DIR_ASM_DMA
+      glds16_asm(arow[i] + (int64_t)i_st * kKStep,
+                 lds + slot * C::SLOT + (wave * C::AI + i) * 64);
+#else
       glds16(arow[i] + (int64_t)i_st * kKStep,
              lds + slot * C::SLOT + (wave * C::AI + i) * 64);
+#endif
+    }
     const bool ok = (tmask >> i_tap) & 1ull;
     const uint16_t* src = ok ? xsrc + (boff + i_toff) : zero;
     // codes of the lane's pixel left in this tap from its first (8-code) group: >= 56 except
@@ -257,13 +266,29 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     if (s + 1 < nsteps) TQ_WAIT_VM(C::LPS);
     else TQ_WAIT_VM(0);
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // ring reads stay behind the barrier
     if (s + 2 < nsteps) issue((slot + 2) % kDirSlots, bnext);
+    compute(slot, bc);
+  };
+  // steady state: every wait and issue unconditional (s + 4 < nsteps), so the compiler's own
+  // wait counts for the fragment registers stay exact across the loop's back edge (with the
+  // conditional issues inside the loop it drained every load in flight once per iteration)
+  auto step_full = [&](int slot, const u32x4 (&bc)[4], u32x4 (&bnext)[4]) {
+    TQ_WAIT_VM(C::LPS);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // ring reads stay behind the barrier
+    issue((slot + 2) % kDirSlots, bnext);
     compute(slot, bc);
   };
   auto run = [&]() {
     issue(0, b0);
     if (nsteps > 1) issue(1, b1);
     int s = 0;
+    for (; s + 4 < nsteps; s += 3) {
+      step_full(0, b0, b2);
+      step_full(1, b1, b0);
+      step_full(2, b2, b1);
+    }
     for (; s + 2 < nsteps; s += 3) {
       step(s, 0, b0, b2);
       step(s + 1, 1, b1, b0);
