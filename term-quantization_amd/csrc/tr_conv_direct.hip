@@ -54,7 +54,10 @@ __device__ unsigned long long g_phase_trace[kTraceMax * 4];
 namespace {
 
 constexpr int kDirThreads = 256;
-constexpr int kDirSlots = 3;  // A ring depth = K-steps in flight + 1
+#ifndef TQ_DIR_DEPTH
+#define TQ_DIR_DEPTH 2  // K-steps of activation fragments / weight images in flight
+#endif
+constexpr int kDirSlots = TQ_DIR_DEPTH + 1;  // A ring depth = K-steps in flight + 1
 
 // MB = 1 or 2: Cout tile BM = 64 MB; the pixel tile is 128 (4 waves x 32 pixels)
 template <int MB>
@@ -259,43 +262,45 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     }
   };
 
-  // Two K-steps in flight: step s is retired by vmcnt(LPS) (only step s + 1 younger), a
-  // barrier makes every wave's A-DMA of step s visible and frees slot (s + 2) % 3.
-  u32x4 b0[4], b1[4], b2[4];
-  auto step = [&](int s, int slot, const u32x4 (&bc)[4], u32x4 (&bnext)[4]) {
-    if (s + 1 < nsteps) TQ_WAIT_VM(C::LPS);
+  // kDirSlots - 1 K-steps in flight: step s is retired by vmcnt((kDirSlots - 2) LPS) (only
+  // the steps issued after it younger), a barrier makes every wave's A-DMA of step s visible
+  // and frees slot (s + kDirSlots - 1) % kDirSlots, which this step refills.
+  constexpr int ND = kDirSlots;
+  u32x4 bb[ND][4];
+  auto step = [&](int s, int slot) {
+    const int younger = nsteps - 1 - s < ND - 2 ? nsteps - 1 - s : ND - 2;
+    if (younger >= 2) TQ_WAIT_VM(2 * C::LPS);
+    else if (younger == 1) TQ_WAIT_VM(C::LPS);
     else TQ_WAIT_VM(0);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // ring reads stay behind the barrier
-    if (s + 2 < nsteps) issue((slot + 2) % kDirSlots, bnext);
-    compute(slot, bc);
+    if (s + ND - 1 < nsteps) issue((slot + ND - 1) % ND, bb[(slot + ND - 1) % ND]);
+    compute(slot, bb[slot]);
   };
-  // steady state: every wait and issue unconditional (s + 4 < nsteps), so the compiler's own
-  // wait counts for the fragment registers stay exact across the loop's back edge (with the
-  // conditional issues inside the loop it drained every load in flight once per iteration)
-  auto step_full = [&](int slot, const u32x4 (&bc)[4], u32x4 (&bnext)[4]) {
-    TQ_WAIT_VM(C::LPS);
+  // steady state: every wait and issue unconditional, so the compiler's own wait counts for
+  // the fragment registers stay exact across the loop's back edge (with conditional issues
+  // inside the loop it drained every load in flight once per iteration)
+  auto step_full = [&](int slot) {
+    TQ_WAIT_VM((ND - 2) * C::LPS);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // ring reads stay behind the barrier
-    issue((slot + 2) % kDirSlots, bnext);
-    compute(slot, bc);
+    issue((slot + ND - 1) % ND, bb[(slot + ND - 1) % ND]);
+    compute(slot, bb[slot]);
   };
   auto run = [&]() {
-    issue(0, b0);
-    if (nsteps > 1) issue(1, b1);
+#pragma unroll
+    for (int i = 0; i < ND - 1; ++i)
+      if (i < nsteps) issue(i, bb[i]);
     int s = 0;
-    for (; s + 4 < nsteps; s += 3) {
-      step_full(0, b0, b2);
-      step_full(1, b1, b0);
-      step_full(2, b2, b1);
+    for (; s + 2 * ND - 2 < nsteps; s += ND) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) step_full(j);
     }
-    for (; s + 2 < nsteps; s += 3) {
-      step(s, 0, b0, b2);
-      step(s + 1, 1, b1, b0);
-      step(s + 2, 2, b2, b1);
+    for (; s < nsteps; s += ND) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j)
+        if (s + j < nsteps) step(s + j, j);
     }
-    if (s < nsteps) step(s, 0, b0, b2);
-    if (s + 1 < nsteps) step(s + 1, 1, b1, b0);
   };
   run();
   if (FLUSH) flush();

@@ -341,7 +341,9 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
       const uint16_t* src = zero;
       if (m < npieces && ir >= 0 && ir < a.H)
         src = xg + (((img * a.H + ir) * W + x) * kStripC + ch * 8);
-      glds16(src, m < npieces ? patch + m * 64 : dummy);
+      // as inline asm: with the builtin, the compiler waited vmcnt(0) before every residual
+      // load's use in the epilogue -- draining the next tile's patch DMA (tq_mfma.h)
+      glds16_asm(src, m < npieces ? patch + m * 64 : dummy);
     }
   };
 
@@ -386,10 +388,12 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
     TQ_WAIT_VM(0);
     sync_target += 4;
     team_sync(ctr, sync_target);
+    asm volatile("" ::: "memory");  // patch reads stay behind the team sync
     // every wave of the team is done with the patch: refill it with the team's next tile
     auto refill = [&]() {
       sync_target += 4;
       team_sync(ctr, sync_target);
+      asm volatile("" ::: "memory");  // every patch read of the team precedes the refill
       if (TQ_ABLATE != 14 && tile + 2 < t_end) issue_patch(tile + 2);
     };
 #if TQ_ABLATE == 12
