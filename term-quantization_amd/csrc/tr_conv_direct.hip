@@ -341,12 +341,17 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
   const bool vec = (a.Cout & 3) == 0;
   const int slot = lane % C::SL;
   const int co = m0 + 4 * slot;
+  // A Cout tile with fewer than BM real channels (MobileNet-V2 / EfficientNet 1x1 convs: Cout
+  // 16, 24, 96 ...): its epilogue packs the valid (pixel, 4-channel slot) pairs onto all 64
+  // lanes instead of leaving the lanes of padding slots idle (Cout 16: 3 of 4 idle).
+  const int vslots = (a.Cout - m0) < C::BM ? (a.Cout - m0 + 3) / 4 : C::SL;  // wave-uniform
+  const bool packed = !DS && vec && vslots < C::SL;
   float4 res[32 / PXI];  // residuals first: their latency overlaps the transpose
 #pragma unroll
   for (int it = 0; it < 32 / PXI; ++it) {
     const int64_t p = wn0 + it * PXI + lane / C::SL;
     res[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (!DS && vec && a.residual && co < a.Cout && p < a.P)
+    if (!DS && !packed && vec && a.residual && co < a.Cout && p < a.P)
       res[it] = *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co);
   }
   __syncthreads();  // every wave is done with the A ring; coef[] is visible
@@ -396,8 +401,35 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     __builtin_amdgcn_wave_barrier();
   }
   put_tile(false);
+  if (packed) {
+    // pair idx -> (pixel idx / vslots, slot idx % vslots); floor(idx * ceil(2^16 / vslots)
+    // / 2^16) is the exact quotient for idx < 32 * 32 and vslots < 128
+    const uint32_t inv = (65536u + vslots - 1) / vslots;
+    for (int idx = lane; idx < 32 * vslots; idx += 64) {
+      const int px = (int)(((uint32_t)idx * inv) >> 16);
+      const int sl = idx - px * vslots;
+      const int64_t p = wn0 + px;
+      if (p >= a.P) continue;
+      const int c4 = m0 + 4 * sl;
+      coef_t psc[4], psh[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        psc[i] = (coef_t)coef[4 * sl + i][0];
+        psh[i] = (coef_t)coef[4 * sl + i][1];
+      }
+      const float4 rv = a.residual
+                            ? *reinterpret_cast<const float4*>(a.residual + p * a.Cout + c4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      const u32x4 v = t[px * C::SL + (sl ^ (px & 15))];
+      const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
+    }
+#if !TQ_PHASE_TRACE
+    return;
+#endif
+  }
 #if TQ_PHASE_TRACE
-  if (co < a.Cout) {
+  if (!packed && co < a.Cout) {
 #else
   if (co >= a.Cout) return;
 #endif
