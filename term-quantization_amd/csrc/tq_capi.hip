@@ -245,8 +245,10 @@ int code_target(const void* codes, int64_t cp, float sf, int32_t bits, int32_t t
 
 // Fill the fused-epilogue fields of `a` from `epi` (shared by both conv engines).
 // Entries of an epilogue code table (tq_device.h kLutMax) for one code target: maxv + 1 when
-// the ReLU fast path applies (relu, 0 < sf < inf) and maxv < kLutMax, else 0 (the kernels
-// compute the codes).  TQ_LUT=0 turns the tables off (A/B, tools only).
+// 0 < sf < inf and maxv < kLutMax (and, where `relu` is required, the values are
+// non-negative), else 0 (the kernels compute the codes).  The conv engines' epilogues take
+// the table for signed values too (tq_device.h lut_codes); the depthwise kernel only after
+// ReLU / ReLU6.  TQ_LUT=0 turns the tables off (A/B, tools only).
 int lut_entries(bool codes, bool relu, double inv, float maxv) {
   static const char* env = getenv("TQ_LUT");
   if (env && atoi(env) == 0) return 0;
@@ -292,8 +294,8 @@ int apply_epilogue(const tq_conv_epilogue* epi, int64_t cout, float* out, int nu
   a->maxv_b = (float)((1u << (epi->codes_b ? epi->bits_b : 0)) - 1u);
   a->k_b = epi->terms_b < 0 ? 0 : epi->terms_b;
   a->fmt_b = epi->fmt_b;
-  a->lut_a = lut_entries(a->codes_a != nullptr, tq::act_nonneg(a->relu), a->inv_a, a->maxv_a);
-  a->lut_b = lut_entries(a->codes_b != nullptr, tq::act_nonneg(a->relu), a->inv_b, a->maxv_b);
+  a->lut_a = lut_entries(a->codes_a != nullptr, true, a->inv_a, a->maxv_a);
+  a->lut_b = lut_entries(a->codes_b != nullptr, true, a->inv_b, a->maxv_b);
   if (epi->config < 0 || epi->config > num_configs || epi->split_k < -1 || epi->split_k > 64)
     return fail(TQ_ERR_INVALID_ARGUMENT, "conv2d: bad config/split_k");
   if (epi->workspace && (uintptr_t)epi->workspace % 16 != 0)

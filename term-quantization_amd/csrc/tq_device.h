@@ -213,6 +213,33 @@ __device__ __forceinline__ void relu_q_epi(const float* y, double inv_sf, float 
 }
 #endif
 
+// Codes of N epilogue values from the code table lut[q] (q <= maxv).  nonneg: the values
+// passed a ReLU / ReLU6 (y >= 0, never NaN).  Otherwise (no activation, swish) the table
+// still applies, as TR is odd in its input: TR(y) = sign(y) TR(|y|) (the reference quantizes
+// |x| and applies the sign, kernels/tr_cuda_kernel.cu:21-23,112), so the code of y < 0 is the
+// table's code of q(|y|) negated -- fp16 sign bit / int16 two's complement, zero stays +0 --
+// and a NaN quantizes to q = 0 (code 0), as tr_value_g1_inv has it.
+template <int N>
+__device__ __forceinline__ void lut_codes(const float* y, double inv_sf, float maxv, int fmt,
+                                          bool nonneg, const uint16_t* lut, uint32_t* bits) {
+  uint32_t q[N];
+  if (nonneg) {
+    relu_q_epi<N>(y, inv_sf, maxv, q);
+  } else {
+    float ay[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) ay[i] = y[i] == y[i] ? fabsf(y[i]) : 0.0f;
+    relu_q_epi<N>(ay, inv_sf, maxv, q);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t v = lut[q[i]];
+    if (!nonneg && y[i] < 0.0f && v != 0u)
+      v = fmt == 1 /* kCodesF16 */ ? (v ^ 0x8000u) : ((0u - v) & 0xFFFFu);
+    bits[i] = v;
+  }
+}
+
 // Fused-epilogue activation (DwConvArgs relu, tq_act_encode_act): 0 none, 1 ReLU, 2 ReLU6,
 // 3 swish y * sigmoid(y) (EfficientNet's MemoryEfficientSwish, with torch's fp32 sigmoid
 // 1 / (1 + exp(-y))).  y becomes the value the next layer's codes encode, o the stored value:

@@ -40,11 +40,8 @@ __device__ __forceinline__ void store_codes4(int16_t* codes, int cp, int cout, i
                                              int k, int fmt, bool relu,
                                              const uint16_t* lut = nullptr) {
   uint32_t v[4];
-  if (lut) {  // the fast path's codes from the LDS table (set only where it applies)
-    uint32_t qv[4];
-    relu_q_epi<4>(y, inv_sf, maxv, qv);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = lut[qv[i]];
+  if (lut) {  // codes from the LDS table (signed values too: tq_device.h lut_codes)
+    lut_codes<4>(y, inv_sf, maxv, fmt, relu, lut, v);
   } else if (relu && inv_sf > 0.0 && inv_sf <= 1.0e308) {  // y >= 0, 0 < sf < inf: fast path
     int32_t t[4];
     tr_values_relu4(y, inv_sf, maxv, relu_peels(maxv, k), t);

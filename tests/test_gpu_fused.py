@@ -205,6 +205,63 @@ def test_schedules_are_bit_identical(layer, cfgs, monkeypatch):
         assert torch.equal(o, o0) and torch.equal(c, c0)
 
 
+@pytest.mark.parametrize("layer", [1, 7, 11])
+def test_signed_code_tables_bit_identical(layer, monkeypatch):
+    """The epilogue code tables for values WITHOUT a ReLU (MobileNet-V2 / EfficientNet project
+    convs, tq_device.h lut_codes: the table's code of q(|y|), negated for y < 0, NaN -> 0)
+    against the VALU engine's computed codes (no tables) and against every MFMA config with the
+    tables off (TQ_LUT=0): outputs and codes bit-identical, with negative, zero, NaN and
+    infinite values (a residual carries the non-finite ones)."""
+    import tq_ops
+    from conftest import RESNET18_TR
+    cin, cout, k, s, hin = RESNET18_TR[layer - 1]
+    batch = 7
+    torch.manual_seed(100 + layer)
+    conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(DEV)
+    x = torch.relu(torch.randn(batch, cin, hin, hin, device=DEV)).to(
+        memory_format=torch.channels_last)
+    ho = (hin + 2 * (k // 2) - k) // s + 1
+    sc = (torch.rand(cout, dtype=torch.float64, device=DEV) - 0.5) * 2e-4
+    sh = torch.randn(cout, dtype=torch.float64, device=DEV) * 0.1
+    res = torch.randn(batch, cout, ho, ho, device=DEV).contiguous(
+        memory_format=torch.channels_last)
+    flat = res.permute(0, 2, 3, 1).view(-1)  # the NHWC storage
+    flat[::97] = float("nan")
+    flat[1::101] = float("inf")
+    flat[2::103] = -float("inf")
+    flat[3::107] = 0.0
+    flat[4::109] = -0.0
+
+    def run(engine, lut, cfg, fmt):
+        monkeypatch.setenv("TQ_CONV_ENGINE", engine)
+        monkeypatch.setenv("TQ_LUT", lut)
+        lay = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+        cp = tq_ops.act_channels(cin)
+        codes = torch.empty((batch, hin, hin, cp), dtype=fmt, device=DEV)
+        tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+        o = torch.full((batch, cout, ho, ho), 7.0, device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        ca = torch.zeros((batch, ho, ho, tq_ops.act_channels(cout)), dtype=fmt, device=DEV)
+        kw = {} if engine == "valu" else {"kc_steps": lay.kc_steps}
+        tq_native.conv2d_termpair_fused(codes, lay.w_codes, cout, k, k, (s, s),
+                                        (k // 2, k // 2), (1, 1), ho, ho, out=o, ch_scale=sc,
+                                        ch_shift=sh, residual=res, relu=False, codes_a=ca,
+                                        quant_a=(0.05, 9, 3), config=cfg, **kw)
+        # codes as the signed integer term sums (fp16 codes are exact integers)
+        return o.view(torch.int32).cpu(), ca.float().cpu()
+
+    o0, c0 = run("valu", "1", 0, torch.int16)
+    assert (c0 < 0).any() and (c0 > 0).any()
+    for cfg in range(0, tq_native.lib().tq_conv2d_mfma_num_configs() + 1):
+        for lut in ("1", "0"):
+            o, c = run("mfma", lut, cfg, torch.float16)
+            assert torch.equal(o, o0) and torch.equal(c, c0), (cfg, lut)
+    # the emitted codes are TR of the stored fp32 values (the oracle's restatement)
+    y = o0.view(torch.float32).permute(0, 2, 3, 1).contiguous()
+    ref = torch.from_numpy(oracle.tr(y.numpy(), 0.05, 9, 1, 3)) / 0.05
+    assert torch.equal(c0[..., :cout], ref.round())
+
+
 @pytest.mark.parametrize("layer,batch", [(8, 5), (13, 8), (13, 37), (16, 8), (19, 3)])
 @pytest.mark.parametrize("cfg", [0, 7, 8])
 def test_patch_streamk_bit_identical(layer, batch, cfg):

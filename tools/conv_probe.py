@@ -28,10 +28,13 @@ def main():
     ap.add_argument("--codes", type=int, default=0, help="next-layer code outputs (0-2)")
     ap.add_argument("--residual", action="store_true", help="fp32 residual input")
     ap.add_argument("--no-out", action="store_true", help="no fp32 output (codes only)")
+    ap.add_argument("--shape", default=None, help="cin,cout,k,stride,hin instead of --layer")
+    ap.add_argument("--no-relu", action="store_true", help="no activation (signed codes)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    cin, cout, k, s, hin = RESNET18_TR[args.layer - 1]
+    cin, cout, k, s, hin = (RESNET18_TR[args.layer - 1] if args.shape is None else
+                            tuple(int(v) for v in args.shape.split(",")))
     args.kc = None
     layer = make_layer(cin, cout, k, s, dev, args)
     cp = tq_ops.act_channels(cin)
@@ -52,7 +55,7 @@ def main():
     q = (0.05, 9, 3)
     fn = lambda: tq_native.conv2d_termpair_fused(
         codes, layer.w_codes, cout, k, k, (s, s), (k // 2, k // 2), (1, 1), ho, ho,
-        out=None if args.no_out else o, ch_scale=sc, ch_shift=sh, residual=res, relu=True,
+        out=None if args.no_out else o, ch_scale=sc, ch_shift=sh, residual=res, relu=not args.no_relu,
         codes_a=ca, quant_a=q if ca is not None else None, codes_b=cb,
         quant_b=q if cb is not None else None,
         workspace=None if layer.engine == "mfma" else ws,

@@ -29,10 +29,12 @@ def main():
     ap.add_argument("--codes", type=int, default=1)
     ap.add_argument("--residual", action="store_true")
     ap.add_argument("--no-out", action="store_true")
+    ap.add_argument("--shape", default=None, help="cin,cout,k,stride,hin instead of --layer")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    cin, cout, k, s, hin = RESNET18_TR[args.layer - 1]
+    cin, cout, k, s, hin = (RESNET18_TR[args.layer - 1] if args.shape is None else
+                            tuple(int(v) for v in args.shape.split(",")))
     args.kc = None
     layer = make_layer(cin, cout, k, s, dev, args)
     cp = tq_ops.act_channels(cin)
