@@ -445,17 +445,24 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   const char* slide_env = getenv("TQ_DW_SLIDE");  // read per launch: tests switch it
   const int slide = slide_env ? atoi(slide_env) : 4;
   // the streaming kernel (default for 3x3 stride 1/2): TQ_DW_STREAM=0 falls back to the
-  // sliding-window / row-blocked kernels (tests and A/B), =6 six rows per block at stride 1
+  // sliding-window / row-blocked kernels (tests and A/B); =8 / =2 eight (four) / two (one)
+  // rows per block at stride 1 (2) instead of the defaults below (A/B)
   const char* stream_env = getenv("TQ_DW_STREAM");
   const int stream_mode = stream_env ? atoi(stream_env) : 1;
   if (stream_mode && a.KH == 3 && a.KW == 3 && a.dh == 1 && a.dw == 1 && a.sh == a.sw &&
       (a.sh == 1 || a.sh == 2) && a.Cp % 4 == 0) {
     const int S = a.sh;
-    const int R = S == 1 ? (stream_mode == 6 ? 6 : 8) : 4;
-    // segments: enough lanes for about two rounds of 2 waves per SIMD, each lane walking
+    // rows per block: fewer rows, fewer VGPRs, more waves.  Stride 1: 4 rows (168 VGPRs, 3
+    // waves per SIMD) on the large maps, 2 below 56 rows; stride 2: 1 row (122 VGPRs, 4
+    // waves).  Each 10-20 % faster than 8 / 4 rows (216 / 203 VGPRs, 2 waves) on the
+    // MobileNet-V2 shapes (profiles/r03ae_dw_probe.txt, r03af_dw_probe.txt).
+    const int R = stream_mode == 8 ? (S == 1 ? 8 : 4)
+                : stream_mode == 2 ? (S == 1 ? 2 : 1)
+                                   : (S == 1 ? (a.Ho >= 56 ? 4 : 2) : 1);
+    // segments: enough lanes for about two rounds of 3 waves per SIMD, each lane walking
     // as many R-row blocks as that leaves (one segment = a whole image column if it fits)
     const int64_t base = (int64_t)a.N * a.Wo * (a.Cp / 4);
-    const int64_t want = (int64_t)device_cus() * 4 * 2 * 64 * 2;
+    const int64_t want = (int64_t)device_cus() * 4 * 3 * 64 * 2;  // 3 waves per SIMD
     const int nblk = (a.Ho + R - 1) / R;
     int64_t nseg = (want + base - 1) / base;
     if (nseg < 1) nseg = 1;
@@ -467,9 +474,15 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
     const int64_t lanes = base * ((a.Ho + seg - 1) / seg);
     const dim3 grid((unsigned)((lanes + 255) / 256));
     const size_t lds = (size_t)a.lut_c * 2;
-    if (S == 2) dwconv3_stream_kernel<2, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
-    else if (R == 6) dwconv3_stream_kernel<1, 6, 4><<<grid, 256, lds, stream>>>(a, seg);
-    else dwconv3_stream_kernel<1, 8, 4><<<grid, 256, lds, stream>>>(a, seg);
+    if (S == 2) {
+      if (R == 1) dwconv3_stream_kernel<2, 1, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else if (R == 2) dwconv3_stream_kernel<2, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else dwconv3_stream_kernel<2, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
+    } else {
+      if (R == 2) dwconv3_stream_kernel<1, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else if (R == 4) dwconv3_stream_kernel<1, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else dwconv3_stream_kernel<1, 8, 4><<<grid, 256, lds, stream>>>(a, seg);
+    }
     return hipGetLastError();
   }
   if (slide && !(rows_env && atoi(rows_env) == 0) && a.KH == 3 && a.KW == 3 && a.dh == 1 &&

@@ -211,7 +211,7 @@ def test_dw_sliding_window_kernel_bit_identical(cfg, relu, monkeypatch):
     outs = []
     # (sliding-window mode, streaming mode, blocks per streaming segment)
     for mode, stream, seg in (("0", "0", "0"), ("4", "0", "0"), ("8", "0", "0"),
-                              ("4", "1", "0"), ("4", "1", "3"), ("4", "6", "2")):
+                              ("4", "1", "0"), ("4", "1", "3"), ("4", "8", "2"), ("4", "2", "3")):
         monkeypatch.setenv("TQ_DW_SLIDE", mode)
         monkeypatch.setenv("TQ_DW_STREAM", stream)
         monkeypatch.setenv("TQ_DW_SEG", seg)
