@@ -59,9 +59,14 @@ __device__ __forceinline__ void dw_emit_coef(const DwConvArgs& a, const uint16_t
     float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
     if (full) {  // a whole chunk inside [0, C), or a pad chunk (nothing to store)
       if (c0 >= a.C) return;
+      if (CPL == 2) {
+        *reinterpret_cast<float2*>(dst) = make_float2(v[0], v[1 % CPL]);
+      } else {
 #pragma unroll
-      for (int i = 0; i < CPL; i += 4)
-        *reinterpret_cast<float4*>(dst + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+        for (int i = 0; i < CPL; i += 4)
+          *reinterpret_cast<float4*>(dst + i) =
+              make_float4(v[i], v[(i + 1) % CPL], v[(i + 2) % CPL], v[(i + 3) % CPL]);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < CPL; ++i)
@@ -93,9 +98,11 @@ __device__ __forceinline__ void dw_emit_coef(const DwConvArgs& a, const uint16_t
       *reinterpret_cast<uint4*>(a.codes + p * a.cp_c + c0) =
           make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4 % CPL] | (v[5 % CPL] << 16),
                      v[6 % CPL] | (v[7 % CPL] << 16));
-    else
+    else if (CPL == 4)
       *reinterpret_cast<uint2*>(a.codes + p * a.cp_c + c0) =
-          make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+          make_uint2(v[0] | (v[1 % CPL] << 16), v[2 % CPL] | (v[3 % CPL] << 16));
+    else
+      *reinterpret_cast<uint32_t*>(a.codes + p * a.cp_c + c0) = v[0] | (v[1 % CPL] << 16);
   }
   if (a.relu || !a.out) return;
   if (a.out_nhwc) {
@@ -325,25 +332,25 @@ __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
   }
 }
 
-// Streaming 3x3 depthwise kernel (dilation 1, stride S = 1 or 2).  A lane owns CPL channels of
-// one output column over a segment of output rows, walked in blocks of R rows: the block's
-// NIN = (R - 1) S + 3 input rows are in registers (three column taps each), the NEXT block's
-// R S new input rows are loaded before the block's MACs and epilogue run, and the block's last
-// 3 - S rows are kept for the next one.  So every input row is loaded once per lane (the
+// Streaming K x K depthwise kernel (K = 3 or 5, dilation 1, stride S = 1 or 2).  A lane owns
+// CPL channels of one output column over a segment of output rows, walked in blocks of R rows:
+// the block's NIN = (R - 1) S + K input rows are in registers (K column taps each), the NEXT
+// block's R S new input rows are loaded before the block's MACs and epilogue run, and the
+// block's last K - S rows are kept for the next one.  So every input row is loaded once per lane (the
 // sliding-window kernel reloads the (3 - S)-row halo of every block), a lane has a block of
 // loads in flight for its whole segment instead of one load-then-compute shot, and the
 // weights and epilogue coefficients are loaded once per segment.  Same exact int32 sums and
 // epilogue as the other depthwise kernels (bit-identical outputs).
-template <int S, int R, int CPL>
-__global__ __launch_bounds__(256) void dwconv3_stream_kernel(DwConvArgs a, int seg) {
+template <int K, int S, int R, int CPL>
+__global__ __launch_bounds__(256) void dwconv_stream_kernel(DwConvArgs a, int seg) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
   if (a.lut_c) {
     lut_build(lut, a.lut_c, a.k_c, a.fmt_c, threadIdx.x, 256);
     __syncthreads();
   }
-  constexpr int NIN = (R - 1) * S + 3;  // input rows of a block
+  constexpr int NIN = (R - 1) * S + K;  // input rows of a block
   constexpr int NEW = R * S;            // rows the next block adds
-  constexpr int KEEP = NIN - NEW;       // rows shared with the next block (3 - S)
+  constexpr int KEEP = NIN - NEW;       // rows shared with the next block (K - S)
   typedef int v4i __attribute__((ext_vector_type(CPL / 2)));  // CPL int16 codes
   const int chunks = a.Cp / CPL;
   const int nseg = (a.Ho + seg - 1) / seg;
@@ -359,31 +366,37 @@ __global__ __launch_bounds__(256) void dwconv3_stream_kernel(DwConvArgs a, int s
   const int oh_begin = sg * seg;
   const int oh_end = oh_begin + seg < a.Ho ? oh_begin + seg : a.Ho;
   const int iw0 = ow * S - a.pw;
-  int w[9][CPL];
+  int w[K * K][CPL];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
+  for (int k = 0; k < K * K; ++k) {
     const int32_t* wt = a.w + (int64_t)k * a.Cp + c0;
+    if (CPL == 2) {
+      const int2 wv = *reinterpret_cast<const int2*>(wt);
+      w[k][0] = sext24(wv.x);
+      w[k][1 % CPL] = sext24(wv.y);
+    } else {
 #pragma unroll
-    for (int i = 0; i < CPL; i += 4) {
-      const int4 wv = *reinterpret_cast<const int4*>(wt + i);
-      w[k][i] = sext24(wv.x);
-      w[k][i + 1] = sext24(wv.y);
-      w[k][i + 2] = sext24(wv.z);
-      w[k][i + 3] = sext24(wv.w);
+      for (int i = 0; i < CPL; i += 4) {
+        const int4 wv = *reinterpret_cast<const int4*>(wt + i);
+        w[k][i] = sext24(wv.x);
+        w[k][(i + 1) % CPL] = sext24(wv.y);
+        w[k][(i + 2) % CPL] = sext24(wv.z);
+        w[k][(i + 3) % CPL] = sext24(wv.w);
+      }
     }
   }
   coef_t sc[CPL], sh[CPL];
   dw_coef<CPL>(a, c0, sc, sh);
-  bool cok[3];
+  bool cok[K];
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) cok[ks] = iw0 + ks >= 0 && iw0 + ks < a.W;
+  for (int ks = 0; ks < K; ++ks) cok[ks] = iw0 + ks >= 0 && iw0 + ks < a.W;
   const int16_t* xb = a.x + (int64_t)img * a.H * a.W * a.Cp + c0;
   const v4i* zero = reinterpret_cast<const v4i*>(&g_dw_zero);
   // unconditional loads: rows outside the image (or wanted == false) read the zero block
-  auto load_row = [&](int ih, bool wanted, v4i (&dst)[3]) {
+  auto load_row = [&](int ih, bool wanted, v4i (&dst)[K]) {
     const bool rok = wanted && ih >= 0 && ih < a.H;
 #pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
+    for (int ks = 0; ks < K; ++ks) {
       const bool ok = rok && cok[ks];
       dst[ks] = *(ok ? reinterpret_cast<const v4i*>(xb + ((int64_t)ih * a.W + iw0 + ks) * a.Cp)
                      : zero);
@@ -391,11 +404,11 @@ __global__ __launch_bounds__(256) void dwconv3_stream_kernel(DwConvArgs a, int s
   };
   const uint16_t* l = a.lut_c ? lut : nullptr;
   int ih0 = oh_begin * S - a.ph;  // first tap row of the block's first output row
-  v4i cur[NIN][3];
+  v4i cur[NIN][K];
 #pragma unroll
   for (int k = 0; k < NIN; ++k) load_row(ih0 + k, true, cur[k]);
   for (int oh0 = oh_begin; oh0 < oh_end; oh0 += R) {
-    v4i nxt[NEW][3];  // the next block's new rows, in flight during this block
+    v4i nxt[NEW][K];  // the next block's new rows, in flight during this block
     const bool more = oh0 + R < oh_end;
 #pragma unroll
     for (int k = 0; k < NEW; ++k) load_row(ih0 + NIN + k, more, nxt[k]);
@@ -405,16 +418,16 @@ __global__ __launch_bounds__(256) void dwconv3_stream_kernel(DwConvArgs a, int s
 #pragma unroll
       for (int i = 0; i < CPL; ++i) acc[i] = 0;
 #pragma unroll
-      for (int kr = 0; kr < 3; ++kr)
+      for (int kr = 0; kr < K; ++kr)
 #pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {
+        for (int ks = 0; ks < K; ++ks) {
           const v4i xv = cur[j * S + kr][ks];
 #pragma unroll
           for (int i = 0; i < CPL / 2; ++i) {
             const int lo = (int)(short)(xv[i] & 0xFFFF);
             const int hi = xv[i] >> 16;
-            acc[2 * i] += lo * w[kr * 3 + ks][2 * i];
-            acc[2 * i + 1] += hi * w[kr * 3 + ks][2 * i + 1];
+            acc[2 * i] += lo * w[kr * K + ks][2 * i];
+            acc[2 * i + 1] += hi * w[kr * K + ks][2 * i + 1];
           }
         }
       const int oh = oh0 + j;
@@ -425,11 +438,11 @@ __global__ __launch_bounds__(256) void dwconv3_stream_kernel(DwConvArgs a, int s
 #pragma unroll
     for (int k = 0; k < KEEP; ++k)
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) cur[k][ks] = cur[NEW + k][ks];
+      for (int ks = 0; ks < K; ++ks) cur[k][ks] = cur[NEW + k][ks];
 #pragma unroll
     for (int k = 0; k < NEW; ++k)
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) cur[KEEP + k][ks] = nxt[k][ks];
+      for (int ks = 0; ks < K; ++ks) cur[KEEP + k][ks] = nxt[k][ks];
     ih0 += NEW;
   }
 }
@@ -449,19 +462,23 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
   // rows per block at stride 1 (2) instead of the defaults below (A/B)
   const char* stream_env = getenv("TQ_DW_STREAM");
   const int stream_mode = stream_env ? atoi(stream_env) : 1;
-  if (stream_mode && a.KH == 3 && a.KW == 3 && a.dh == 1 && a.dw == 1 && a.sh == a.sw &&
-      (a.sh == 1 || a.sh == 2) && a.Cp % 4 == 0) {
+  const char* s5_env = getenv("TQ_DW_STREAM5");  // 5x5 on the streaming kernel (1: on)
+  const bool s5 = s5_env && atoi(s5_env) != 0;
+  if (stream_mode && a.KH == a.KW && (a.KH == 3 || (a.KH == 5 && s5)) && a.dh == 1 &&
+      a.dw == 1 && a.sh == a.sw && (a.sh == 1 || a.sh == 2) && a.Cp % 4 == 0) {
     const int S = a.sh;
     // rows per block: fewer rows, fewer VGPRs, more waves.  Stride 1: 4 rows (168 VGPRs, 3
     // waves per SIMD) on the large maps, 2 below 56 rows; stride 2: 1 row (122 VGPRs, 4
     // waves).  Each 10-20 % faster than 8 / 4 rows (216 / 203 VGPRs, 2 waves) on the
     // MobileNet-V2 shapes (profiles/r03ae_dw_probe.txt, r03af_dw_probe.txt).
-    const int R = stream_mode == 8 ? (S == 1 ? 8 : 4)
+    const int R = a.KH == 5 ? (S == 1 && stream_mode == 8 ? 2 : 1)  // 5x5: 1 row (2: A/B)
+                : stream_mode == 8 ? (S == 1 ? 8 : 4)
                 : stream_mode == 2 ? (S == 1 ? 2 : 1)
                                    : (S == 1 ? (a.Ho >= 56 ? 4 : 2) : 1);
     // segments: enough lanes for about two rounds of 3 waves per SIMD, each lane walking
     // as many R-row blocks as that leaves (one segment = a whole image column if it fits)
-    const int64_t base = (int64_t)a.N * a.Wo * (a.Cp / 4);
+    const int cpl = a.KH == 5 ? 2 : 4;  // channels per lane
+    const int64_t base = (int64_t)a.N * a.Wo * (a.Cp / cpl);
     const int64_t want = (int64_t)device_cus() * 4 * 3 * 64 * 2;  // 3 waves per SIMD
     const int nblk = (a.Ho + R - 1) / R;
     int64_t nseg = (want + base - 1) / base;
@@ -474,14 +491,20 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
     const int64_t lanes = base * ((a.Ho + seg - 1) / seg);
     const dim3 grid((unsigned)((lanes + 255) / 256));
     const size_t lds = (size_t)a.lut_c * 2;
-    if (S == 2) {
-      if (R == 1) dwconv3_stream_kernel<2, 1, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else if (R == 2) dwconv3_stream_kernel<2, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else dwconv3_stream_kernel<2, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
+    if (a.KH == 5) {
+      // two channels per lane (4-byte loads): the 25 taps' weights of four channels would
+      // take 100 VGPRs
+      if (S == 2) dwconv_stream_kernel<5, 2, 1, 2><<<grid, 256, lds, stream>>>(a, seg);
+      else if (R == 2) dwconv_stream_kernel<5, 1, 2, 2><<<grid, 256, lds, stream>>>(a, seg);
+      else dwconv_stream_kernel<5, 1, 1, 2><<<grid, 256, lds, stream>>>(a, seg);
+    } else if (S == 2) {
+      if (R == 1) dwconv_stream_kernel<3, 2, 1, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else if (R == 2) dwconv_stream_kernel<3, 2, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else dwconv_stream_kernel<3, 2, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
     } else {
-      if (R == 2) dwconv3_stream_kernel<1, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else if (R == 4) dwconv3_stream_kernel<1, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else dwconv3_stream_kernel<1, 8, 4><<<grid, 256, lds, stream>>>(a, seg);
+      if (R == 2) dwconv_stream_kernel<3, 1, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else if (R == 4) dwconv_stream_kernel<3, 1, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
+      else dwconv_stream_kernel<3, 1, 8, 4><<<grid, 256, lds, stream>>>(a, seg);
     }
     return hipGetLastError();
   }

@@ -225,3 +225,43 @@ def test_dw_sliding_window_kernel_bit_identical(cfg, relu, monkeypatch):
     for o, nc in outs[1:]:
         assert torch.equal(o, outs[0][0]) and torch.equal(nc, outs[0][1])
     assert not torch.isnan(outs[0][0].view(torch.float32)).any()
+
+
+@pytest.mark.parametrize("cfg", [
+    # c, hw, stride, (pad top, pad left), ho: 5x5 pad 2 (EfficientNet stride 1), static-same
+    # stride 2 on even / odd inputs (pad 1 before, 2 / 1 after), partial channel chunks
+    (40, 28, 1, (2, 2), 28), (120, 14, 1, (2, 2), 14), (240, 28, 2, (1, 1), 14),
+    (144, 15, 2, (2, 2), 8), (20, 9, 1, (2, 2), 9), (672, 7, 1, (2, 2), 7),
+])
+@pytest.mark.parametrize("relu", [6, "swish"])
+def test_dw5_streaming_kernel_bit_identical(cfg, relu, monkeypatch):
+    """The streaming depthwise kernel at 5x5 (two channels per lane, one or two output rows per
+    block, one- and multi-block segments) against the row-blocked 5x5 kernel (TQ_DW_STREAM=0):
+    bit-identical fp32 outputs and next-layer codes, for stride 1 and static-same stride 2."""
+    import tq_native
+    c, hw, s, (pt, pl), ho = cfg
+    torch.manual_seed(c + hw + 5)
+    conv = nn.Conv2d(c, c, 5, s, 2, groups=c, bias=False)
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 16, 1, 16)
+    cp = layer.act_channels
+    x = torch.relu(torch.randn(3, c, hw, hw, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.zeros((3, hw, hw, cp), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    sc = torch.rand(c, dtype=torch.float64, device=DEV) * 1e-5
+    sh = torch.randn(c, dtype=torch.float64, device=DEV) * 0.1
+    outs = []
+    monkeypatch.setenv("TQ_DW_STREAM5", "1")
+    for stream, seg in (("0", "0"), ("1", "0"), ("1", "3"), ("8", "0"), ("8", "2")):
+        monkeypatch.setenv("TQ_DW_STREAM", stream)
+        monkeypatch.setenv("TQ_DW_SEG", seg)
+        o = torch.full((3, c, ho, ho), float("nan"), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        nc = torch.full((3, ho, ho, cp), -1, dtype=torch.int16, device=DEV)
+        tq_native.dwconv2d_termpair_fused(codes, c, layer.w_codes, 5, 5, (s, s), (pt, pl),
+                                          (1, 1), ho, ho, sc, sh, relu, out=o, next_codes=nc,
+                                          quant=(0.03, 9, 3))
+        outs.append((o.view(torch.int32).cpu(), nc.cpu()))
+    for o, nc in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(nc, outs[0][1])
+    assert not torch.isnan(outs[0][0].view(torch.float32)).any()

@@ -1,6 +1,6 @@
+#!/bin/bash
+# Fused MobileNet-V2 / EfficientNet-b0 images/s and per-kernel averages (bench_d4.cnn_fused)
 set -u
-timeout -k 10 600 python -u -m pytest tests/test_gpu_models.py -k dw -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03ag_tests.log 2>&1 || { tail -30 gpurun_out/r03ag_tests.log; exit 1; }
-tail -1 gpurun_out/r03ag_tests.log
 timeout -k 10 300 python -c "
 import sys, json, torch; sys.path.insert(0, 'tools'); import bench_d4
 dev = torch.device('cuda:0')
