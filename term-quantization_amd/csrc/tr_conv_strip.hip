@@ -130,8 +130,14 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
     const uint16_t* lut = side ? lut_b : lut_a;
     const int fmt = side ? a.fmt_b : a.fmt_a;
     uint32_t bits[4];
-    if (lut) {  // codes from the LDS table (signed values too: tq_device.h lut_codes)
-      lut_codes<4>(y, inv, maxv, fmt, act_nonneg(a.relu), lut, bits);
+    // the code table after a ReLU only: the signed-value variant (tq_device.h lut_codes) put
+    // this engine over its register budget (scratch spills: 127 -> 177 us, r03ai); without a
+    // ReLU the codes are computed
+    if (lut && act_nonneg(a.relu)) {
+      uint32_t qv[4];
+      relu_q_epi<4>(y, inv, maxv, qv);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bits[e] = lut[qv[e]];
     } else {
       int32_t v[4];
       if (side ? ep.fast_b : ep.fast_a) {
