@@ -1,6 +1,8 @@
 """ResNet-18 TQ (g=8, alpha=k=12, wb=db=9, dt=3) inference throughput on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256]
+        (N > 1 without a launcher: bench.py starts N fresh rank processes itself, before any
+        GPU call, rendezvous on 127.0.0.1)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -50,7 +52,7 @@ MFMA_F16_PEAK_TFLOPS = 2500.0
 FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 vector / f32-MFMA peak (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -80,7 +82,50 @@ def parse():
     ap.add_argument("--unfused", action="store_true",
                     help="run the module path (separate BN/ReLU/add/TR passes) instead of "
                          "the fused executor")
-    return ap.parse_args()
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher check only (tests): each rank prints its rank and world "
+                         "size as JSON and exits before touching the GPU")
+    return ap.parse_args(argv)
+
+
+def launch_plan(gpus, env):
+    """What this process does for ``--gpus N`` given the environment: ("spawn", N) when no
+    launcher set WORLD_SIZE and N > 1 (this process starts N fresh rank processes before any
+    GPU call), ("run", world) when WORLD_SIZE agrees with N (or N = 1 without a launcher),
+    else ("error", message): a mismatch never silently measures another GPU count."""
+    if gpus < 1:
+        return ("error", "--gpus must be >= 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("spawn", gpus) if gpus > 1 else ("run", 1)
+    if int(ws) != gpus:
+        return ("error", "--gpus %d but WORLD_SIZE=%s: launch with --nproc-per-node %d, or "
+                         "without a launcher to let bench.py start the ranks" % (gpus, ws, gpus))
+    return ("run", gpus)
+
+
+def spawn_ranks(argv, n, dry):
+    """Start ranks 0..n-1 as fresh processes (this one has not touched the GPU: only
+    torch.cuda.device_count(), which does not initialise it on this image), one per GPU,
+    rendezvous on 127.0.0.1; return non-zero if any rank fails."""
+    import socket
+    import subprocess
+    if not dry:
+        have = torch.cuda.device_count()
+        if have < n:
+            print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, have), file=sys.stderr)
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return 0 if all(rc == 0 for rc in rcs) else 1
 
 
 class KernelTimer(object):
@@ -311,11 +356,22 @@ def d1_tr_op(dev, iters=20):
             "hbm_frac": gbs / HBM_PEAK_GBS, "bytes_per_element": 8, "launches": iters}
 
 
-def main():
-    args = parse()
-    os.environ["TQ_CONV_ENGINE"] = args.engine
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    what, val = launch_plan(args.gpus, os.environ)
+    if what == "error":
+        print("bench.py: " + val, file=sys.stderr)
+        return 2
+    if what == "spawn":
+        return spawn_ranks(argv, val, args.dry_launch)
+    world = val
     rank = int(os.environ.get("RANK", "0"))
+    if args.dry_launch:
+        print(json.dumps({"rank": rank, "world_size": world,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}))
+        return 0
+    os.environ["TQ_CONV_ENGINE"] = args.engine
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -578,7 +634,8 @@ def main():
         dist.destroy_process_group()
     if result is not None:
         print(json.dumps(result))
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

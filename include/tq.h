@@ -385,7 +385,7 @@ int tq_lstm_cell_f32(const float *gx, const float *hh, float *c, float *h, int64
  * device buffers; c_out = c_{steps-1} (h_{steps-1} is out[steps-1]); out and c_out may not
  * alias h0 / c0.  `workspace`: tq_lstm_seq_workspace_bytes(batch, hidden) device bytes (0 in
  * this version; < 0: the shape is outside the domain -- hidden <= 1024 and the batch's hidden
- * state staged in one workgroup's LDS, e.g. batch <= 32 at hidden 650).  fp32 arithmetic, a
+ * state staged in one workgroup's LDS, e.g. batch <= 39 at hidden 650).  fp32 arithmetic, a
  * fixed summation order.
  */
 int64_t tq_lstm_seq_workspace_bytes(int64_t batch, int64_t hidden);

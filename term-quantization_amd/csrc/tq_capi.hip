@@ -250,7 +250,7 @@ int code_target(const void* codes, int64_t cp, float sf, int32_t bits, int32_t t
 // the table for signed values too (tq_device.h lut_codes); the depthwise kernel only after
 // ReLU / ReLU6.  TQ_LUT=0 turns the tables off (A/B, tools only).
 int lut_entries(bool codes, bool relu, double inv, float maxv) {
-  static const char* env = getenv("TQ_LUT");
+  const char* env = getenv("TQ_LUT");  // read per call: tests switch it
   if (env && atoi(env) == 0) return 0;
   if (!codes || !relu || !(inv > 0.0 && inv <= 1.0e308)) return 0;
   const int n = (int)maxv + 1;

@@ -164,11 +164,14 @@ __device__ __forceinline__ uint32_t relu_q(float y, double inv_sf, float maxv) {
   return (uint32_t)r + (__builtin_amdgcn_fractf(r) >= 0.5f ? 1u : 0u);
 }
 
-// Epilogue arithmetic of the term-pair kernels (TQ_EPI_F32, default 1: fp32).
-//   fold_acc: y = fp32(acc * sc + sh) of the exact integer sum -- in fp32 (one fma of the
-//     int -> fp32 converted sum, |error| <= ~3 ulp of max(|acc sc|, |y|), far inside the 1e-5
-//     parity bound) instead of fp64 (6 fp64-rate operations per value); every engine uses the
-//     same fold, so their outputs stay bit-identical.
+// Epilogue arithmetic of the term-pair kernels (TQ_EPI_F32, default 0: the fp64 fold ships;
+// 1 is an A/B build, measured no faster).
+//   fold_acc: y = fp32(acc * sc + sh) of the exact integer sum -- with TQ_EPI_F32=1 in fp32
+//     (one fma of the int -> fp32 converted sum: (float)acc is itself inexact once |acc| >=
+//     2^24, which the int32 sums allow up to 2^31, so the error bound is ~3 ulp of
+//     max(|acc sc|, |y|) plus that conversion's half ulp of |acc sc|, still far inside the
+//     1e-5 parity bound) instead of fp64 (6 fp64-rate operations per value); every engine uses
+//     the same fold, so their outputs stay bit-identical.
 //   relu_q_epi: relu_q (q = round(fp32(y / sf)), exact as the reference rounds) from an fp32
 //     product y * fp32(1/sf): |r_fast - fp32(y / sf)| <= 3 * 2^-24 r, so the rounded integer
 //     can differ only when r_fast lies within that of a half-integer; those values (about

@@ -207,9 +207,12 @@ static int64_t lstm_seg_len(int64_t H) {
 
 // 0 (no workspace) when the step kernel's LDS holds the shape, else -1 (unsupported).
 int64_t lstm_seq_workspace_bytes(int64_t B, int64_t H) {
+  // one cell thread per (batch row, unit) and 16 dot-product threads per gate row of a unit
+  static_assert(4 * 4 * kStepSeg <= kStepThreads, "4 gate rows x nu <= 4 units of dot threads");
   const int64_t L = lstm_seg_len(H);
   if (B < 1 || H < 1 || L == 0) return -1;
   const int64_t HP = kStepSeg * L, nu = (H + 255) / 256;
+  if (B * nu > kStepThreads) return -1;
   const int64_t lds = (B * HP + 4 * nu * HP + 4 * nu * B * kStepSeg) * 4;
   return lds <= 160 * 1024 ? 0 : -1;
 }

@@ -474,7 +474,7 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
 }
 
 // ---------------------------------------------------------------------------------------
-// Pointwise engine: 1x1 convs (pad 0, any stride) with K <= 4 K-steps (Cin <= 256): the
+// Pointwise engine: 1x1 convs (pad 0, any stride) with K <= 3 K-steps (Cin <= 192): the
 // MobileNet-V2 / EfficientNet expand and project convs and the ResNet downsamples.  Their
 // tiles are mostly epilogue (1-4 K-steps of MFMA, then 8192 outputs), so one tile per
 // workgroup leaves each workgroup's lifetime to fixed latencies (weight DMA, fragment loads,
@@ -711,7 +711,7 @@ hipError_t launch_conv2d_pw(const ConvArgs& a, hipStream_t stream) {
     case 1: return sw ? launch_pw_cfg<1, true>(a, stream) : launch_pw_cfg<1, false>(a, stream);
     case 2: return sw ? launch_pw_cfg<2, true>(a, stream) : launch_pw_cfg<2, false>(a, stream);
     case 3: return sw ? launch_pw_cfg<3, true>(a, stream) : launch_pw_cfg<3, false>(a, stream);
-    default: return sw ? launch_pw_cfg<4, true>(a, stream) : launch_pw_cfg<4, false>(a, stream);
+    default: return hipErrorInvalidValue;  // conv_pw_eligible: 1..3 K-steps only
   }
 }
 

@@ -479,14 +479,16 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // stride 1, KH*KW >= 2, NHWC out; else the gather default).
 // 9-10 direct (tr_conv_direct.hip: Cp % 64 == 0, NHWC out; 128 x 128 / 64 x 128 tiles).
 // 11 row strip (tr_conv_strip.hip: 3x3/1, 64 -> 64 channels, W <= 56; else the default).
-int conv_mfma_num_configs() { return 12; }
+// 12 persistent pointwise (tr_conv_direct.hip: 1x1, K <= 3 K-steps; else the default).
+// 13 tap ring (tr_conv_ring.hip: 3x3/1 "same", Cp % 64 == 0, Wo <= 256; else the default).
+int conv_mfma_num_configs() { return 13; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
   ConvArgs a = a_in;
   // Tile order: with the Cout tile as the slow index, an XCD's contiguous run of tiles
   // shares one weight slice in its L2 (speed only).  TQ_MSLOW=0/1 overrides (A/B).
-  static const char* ms = getenv("TQ_MSLOW");
+  const char* ms = getenv("TQ_MSLOW");  // read per launch: tests switch it
   a.m_slow = ms ? atoi(ms) : 0;
   const bool pipe_ok = a.Cp % kKStep == 0 && a.KH * a.KW <= 64;
   int cfg = a.config > 0 ? a.config - 1 : -1;
@@ -509,6 +511,11 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
     return launch_conv2d_direct(a, 1, stream);
   }
+  // tap-ring engine: config 13, or TQ_RING=1 (read per launch: tests switch it)
+  const char* ring = getenv("TQ_RING");
+  if ((cfg == 12 || (cfg < 0 && ring && atoi(ring) == 1)) && conv_ring_eligible(a, out_nhwc))
+    return launch_conv2d_ring(a, stream);
+  if (cfg == 12) cfg = -1;
   static const char* strip = getenv("TQ_STRIP");  // A/B override (tools only): 0 off
   if (cfg == 10 || (cfg < 0 && !(strip && atoi(strip) == 0))) {
     if (conv_strip_eligible(a, out_nhwc)) return launch_conv2d_strip(a, stream);

@@ -1,0 +1,619 @@
+// Term-pair Conv2d on the matrix cores, tap-ring engine: 3x3 stride-1 convs with Cp % 64 == 0
+// and Cout >= 128 (ResNet-18 layer2/3/4 3x3 convs), persistent workgroups that stream K-steps
+// across tiles without refilling the pipeline.
+//
+// Same exact arithmetic as the other MFMA engines (tr_conv_mfma.hip): fp16 term-sum codes,
+// v_mfma_f32_32x32x16_f16, fp32 partial sums that stay exact integers inside host-bounded
+// windows, moved into int32 sums at every window end, one fp64 fold in the shared epilogue.
+//
+// Why another engine.  The input-patch engine (tr_conv_patch.hip) has the right data flow --
+// activations staged once per 64-channel chunk as an LDS patch that all nine taps read, weight
+// K-steps through an LDS-DMA ring -- but its K loop spends ~3500 cycles per K-step against
+// 1024 of matrix-core work (r03m counters: 164 VALU, 121 SALU and 26 branches per wave and
+// step: a runtime division per weight issue, a binary search for every counted wait, dynamic
+// ring and patch indices), reads each step's fragments only after that step's barrier, and
+// pays a pipeline fill for every tile.  Here:
+//   * the nine taps of a chunk are unrolled and the ring has 3 slots, so every ring slot, LDS
+//     offset and vmcnt count is a compile-time constant (9 % 3 == 0: step (c, t) uses slot t%3);
+//   * the barrier at the top of step s retires step s+1's weight image (issued two steps
+//     earlier), so each wave reads step s+1's first fragments during step s's last MFMAs --
+//     fragment reads run one 16-code substep ahead of the MFMAs, across step boundaries;
+//   * the patch rows use a 144-byte pixel pitch (128 B of codes + 16 B pad): the 16 lanes of a
+//     ds_read_b128 group read 16 distinct pixels whose 16-byte chunks land in 16 distinct bank
+//     quads (pitch 9 units, odd), with no XOR -- a step's four substep reads of one B block are
+//     one address + immediate offsets 0/32/64/96;
+//   * tiles are R whole output rows (R * Wo <= 256 pixels), so a patch is at most R + 2 input
+//     rows, and the next chunk's patch -- the next tile's first chunk at a tile's end -- is
+//     issued one 1 KB piece per wave and step at taps 0..PI-1 of the current chunk;
+//   * workgroups are persistent (one per CU, XCD-aware tile order): the weight ring and the
+//     patch stream run straight through tile boundaries; the epilogue works from the MFMA
+//     register layout (no LDS transpose), so it never waits for the next tile's staging.
+//
+//   workgroup = 8 waves (2 along Cout x 4 along pixels), tile 128 (Cout) x 256 (pixel columns,
+//               R * Wo of them real); wave tile 64 x 64 = 2 x 2 blocks of 32 x 32
+//   K order   = chunk-major, tap-minor (as the patch engine: kc_chunk windows apply)
+//   LDS       = [3][128 rows][128 B] weight ring (rows swizzled chunk ^= (row >> 1) & 7 on the
+//               source side) | [2][8 * PI KB] patches (144 B per pixel) | one zero pixel |
+//               [Cout][2] fp64 epilogue coefficients | epilogue code tables
+#include <stdlib.h>
+
+#include "tq_device.h"
+#include "tq_epilogue.h"
+#include "tq_launch.h"
+#include "tq_mfma.h"
+
+#ifndef RING_AB
+#define RING_AB 0  // timing-only ablation builds (tools/variant.sh); 0 = the product kernel
+#endif
+
+namespace tq {
+
+namespace {
+
+constexpr int kRingThreads = 512;
+constexpr int kRingBM = 128;            // Cout rows per tile
+constexpr int kRingBN = 256;            // pixel columns per tile
+constexpr int kRingSlot = kRingBM * 128;  // bytes per ring slot
+constexpr int kPitch = 144;             // patch bytes per pixel
+constexpr int kRingTaps = 9;            // 3 x 3
+
+__host__ __device__ constexpr int ring_pbuf(int pi) { return 8 * pi * 1024; }
+__host__ __device__ constexpr int ring_pxs(int pi) { return ring_pbuf(pi) / kPitch; }
+__host__ __device__ constexpr int ring_patch_off(int nr) { return nr * kRingSlot; }
+__host__ __device__ constexpr int ring_zero_off(int pi, int nr) {
+  return ring_patch_off(nr) + 2 * ring_pbuf(pi);
+}
+__host__ __device__ constexpr int ring_coef_off(int pi, int nr) {
+  return ring_zero_off(pi, nr) + 160;
+}
+// Weight ring depth for a patch of PI pieces per wave: as deep as the 160 KB of LDS allows
+// (3 x 16 KB beside two 48 KB patch buffers ... 6 beside two 24 KB ones).  The barrier of
+// step s retires step s+1's image, issued at step s+2-NR: NR-2 steps of DMA lead.
+__host__ __device__ constexpr int ring_slots(int pi) { return pi >= 6 ? 3 : pi == 5 ? 4 : pi == 4 ? 5 : 6; }
+
+// The rows of one tile and the input rows its patch holds.
+struct RingTile {
+  int64_t p0;     // first output pixel
+  int m0;         // first Cout row
+  int64_t base;   // first flattened input row (img * H + iy) of the patch
+  int px;         // patch pixels (rows * W)
+};
+
+__host__ __device__ inline RingTile ring_tile(const ConvArgs& a, int64_t tile, int R, int mt,
+                                              int m_slow, int64_t pt_count) {
+  RingTile t;
+  const int64_t pt = m_slow ? tile % pt_count : tile / mt;
+  const int m = (int)(m_slow ? tile / pt_count : tile % mt);
+  t.m0 = m * kRingBM;
+  const int64_t nrows = (int64_t)a.N * a.Ho;
+  const int64_t gr0 = pt * R;
+  const int64_t gr1 = (gr0 + R < nrows ? gr0 + R : nrows) - 1;
+  t.p0 = gr0 * a.Wo;
+  const int64_t img0 = gr0 / a.Ho, img1 = gr1 / a.Ho;
+  const int oy0 = (int)(gr0 - img0 * a.Ho), oy1 = (int)(gr1 - img1 * a.Ho);
+  int r0 = oy0 - a.ph;
+  int r1 = oy1 - a.ph + (a.KH - 1);
+  r0 = r0 < 0 ? 0 : r0;
+  r1 = r1 > a.H - 1 ? a.H - 1 : r1;
+  t.base = img0 * a.H + r0;
+  t.px = (int)((img1 * a.H + r1 - t.base + 1) * a.W);
+  return t;
+}
+
+// One LDS-DMA wave-instruction (1 KB, lane-linear destination), issued as inline asm so the
+// compiler's own wait counts stay exact (tq_mfma.h glds16_asm); the LDS address is uniform.
+__device__ __forceinline__ void ring_dma(const void* src, uint32_t lds_byte) {
+  if (RING_AB == 3) return;  // timing only: nothing staged
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(lds_byte)
+               : "memory", "m0");
+}
+
+// compile-time loop: f(ic<I>) for I in [I0, N)
+template <int V>
+struct ic {
+  static constexpr int value = V;
+};
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(ic<I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+__device__ __forceinline__ half8 lds_frag(uint32_t byte_addr) {
+  return __builtin_bit_cast(
+      half8, *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(
+                 (uintptr_t)byte_addr));
+}
+
+// FAST: the fused ResNet executor's epilogue form, specialised at launch -- ReLU, fp16 codes
+// from the code tables (every code output has one), Cout % 4 == 0 -- with per-pixel base
+// pointers and compile-time channel offsets; other forms run the shared emit4_nhwc_res.
+template <int PI, bool FLUSH, bool FAST>
+__global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArgs a, int R,
+                                                                        int64_t ptc) {
+  constexpr int NR = ring_slots(PI);
+  // the next chunk's last patch piece (tap PI-1) must be older than the weight image the
+  // barrier of that chunk's last step retires (issued at tap 10-NR)
+  static_assert(PI <= 10 - NR, "patch pieces must land before the chunk switch");
+  extern __shared__ __attribute__((aligned(16))) u32x4 ring_lds[];
+  const uint32_t lds0 =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)ring_lds;
+  constexpr uint32_t kPatchOff = ring_patch_off(NR);
+  constexpr uint32_t kZeroOff = ring_zero_off(PI, NR);
+  double* coef = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(ring_lds) +
+                                           ring_coef_off(PI, NR));
+  uint16_t *lut_a, *lut_b;
+  conv_luts(a, reinterpret_cast<uint16_t*>(coef + 2 * a.Cout), lut_a, lut_b);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int hh = lane >> 5;
+  const int wm = (wave >> 2) * 64;  // this wave's Cout rows [wm, wm + 64) of the tile
+  const int wn = (wave & 3) * 64;   // and pixel columns [wn, wn + 64)
+  const int mt = (a.Cout + kRingBM - 1) / kRingBM;
+  const int64_t T = ptc * mt;
+  const int64_t G = gridDim.x;
+  const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
+  const int BNv = R * a.Wo;
+  const int nch = a.Cp / kKStep;
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
+  const char* __restrict__ wgb = reinterpret_cast<const char*>(a.w);
+  const char* zsrc = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
+
+  // epilogue coefficients of every channel, the zero pixel
+  for (int i = tid; i < a.Cout; i += kRingThreads) {
+    coef[2 * i] = a.ch_scale ? a.ch_scale[i] : a.scale;
+    coef[2 * i + 1] = a.ch_scale ? a.ch_shift[i] : (a.bias ? (double)a.bias[i] : 0.0);
+  }
+  if (tid < kPitch / 16)
+    *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(ring_lds) + kZeroOff + tid * 16) =
+        (u32x4)0u;
+
+  // ---- weight DMA: wave w moves rows [16 w, 16 w + 16) of a slot in 2 instructions of 8 rows
+  int64_t wlane[2];  // per-lane byte offset of its 16-byte source chunk within a K column
+  uint32_t wdst[2];  // LDS byte offset of the instruction within a slot
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave * 2 + i) * 8 + (lane >> 3);
+    wlane[i] = (int64_t)r * a.Kp * 2 + (((lane & 7) ^ ((r >> 1) & 7)) * 16);
+    wdst[i] = (uint32_t)((wave * 2 + i) * 1024);
+  }
+  // weight image of K-step (tap t, chunk c) of the tile whose first row is m0 into `slot`
+  auto issue_w = [&](int m0, int t, int c, int slot, bool live, uint32_t soff = 0)
+      __attribute__((always_inline)) {
+    const int64_t col = ((int64_t)m0 * a.Kp + (int64_t)t * a.Cp + (int64_t)c * kKStep) * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      ring_dma(live ? wgb + col + wlane[i] : zsrc, lds0 + slot * kRingSlot + soff + wdst[i]);
+  };
+
+  // ---- patch DMA: piece j of wave w = LDS bytes [(w PI + j) KB, +1 KB) of a patch buffer;
+  // lane byte b = that + 16 lane -> pixel b / 144, 16-byte chunk (b % 144) / 16 (8 = pad)
+  // per piece: the lane's pixel (or PXS + 1 for a pad chunk: never below any px) and its
+  // 32-bit byte offset from the chunk's first patch pixel; no branch at issue time
+  int ppix[PI];
+  uint32_t poff[PI];
+#pragma unroll
+  for (int j = 0; j < PI; ++j) {
+    const int b = (wave * PI + j) * 1024 + lane * 16;
+    const int q = b / kPitch, ch = (b - q * kPitch) >> 4;
+    ppix[j] = ch < 8 ? q : 1 << 20;
+    poff[j] = (uint32_t)((q * a.Cp + ch * 8) * 2);
+  }
+  // src0: byte address of the chunk's first patch pixel, channel chunk c (uniform)
+  auto issue_piece = [&](int j, const char* src0, int px, int buf)
+      __attribute__((always_inline)) {
+    const char* src = ppix[j] < px ? src0 + poff[j] : zsrc;
+    ring_dma(src, lds0 + kPatchOff + buf * ring_pbuf(PI) + (wave * PI + j) * 1024);
+  };
+
+  // ---- B fragment pixels of the current tile: patch pixel of tap (0, 0) and in-bounds taps
+  int pix[2];
+  uint32_t tmask[2];
+  auto setup_b = [&](const RingTile& tl) __attribute__((always_inline)) {
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+      const int j = wn + 32 * bn + r32;
+      const int64_t p = tl.p0 + j;
+      pix[bn] = 0;
+      tmask[bn] = 0;
+      if (j < BNv && p < a.P) {
+        const int64_t img = p / HoWo;
+        const int rem = (int)(p - img * HoWo);
+        const int oy = rem / a.Wo;
+        const int ox = rem - oy * a.Wo;
+        const int iy0 = oy - a.ph, ix0 = ox - a.pw;
+        pix[bn] = (int)((img * a.H + iy0 - tl.base) * a.W + ix0);
+#pragma unroll
+        for (int t = 0; t < kRingTaps; ++t) {
+          const int iy = iy0 + t / 3, ix = ix0 + t % 3;
+          if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) tmask[bn] |= 1u << t;
+        }
+      }
+    }
+  };
+  // LDS byte address of B block bn's substep-0 fragment at tap t of the patch in buffer buf
+  auto baddr = [&](int bn, int t, int buf) __attribute__((always_inline)) {
+    const uint32_t in = lds0 + kPatchOff + buf * ring_pbuf(PI) +
+                        (uint32_t)(pix[bn] + (t / 3) * a.W + (t % 3)) * kPitch + hh * 16;
+    const uint32_t zero = lds0 + kZeroOff + hh * 16;
+    return ((tmask[bn] >> t) & 1u) ? in : zero;
+  };
+  // A fragment byte address (slot 0) of block bm, substep k: swizzled row image
+  uint32_t aaddr[2][4];
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = wm + 32 * bm + r32;
+      aaddr[bm][k] = lds0 + (uint32_t)(row * 128 + (((2 * k + hh) ^ ((row >> 1) & 7)) * 16));
+    }
+
+  // ---- the tile stream
+  int64_t tile = g;
+  RingTile cur = ring_tile(a, tile, R, mt, a.m_slow, ptc);
+  int64_t ntile = tile + G;
+  RingTile nxt = ring_tile(a, ntile < T ? ntile : tile, R, mt, a.m_slow, ptc);
+  setup_b(cur);
+  // prologue: chunk 0's patch into buffer 0, weight images of steps 0 .. NR-2
+#pragma unroll
+  for (int j = 0; j < PI; ++j)
+    issue_piece(j, reinterpret_cast<const char*>(xg + cur.base * a.W * a.Cp), cur.px, 0);
+#pragma unroll
+  for (int j = 0; j + 1 < NR; ++j) issue_w(cur.m0, j, 0, j, true);
+  TQ_WAIT_VM(0);
+  __syncthreads();  // coefficients, tables, zero pixel, the first images visible
+  // ring slot of the current chunk's tap 0 (the stream's step index mod NR; 0 when NR | 9)
+  int sbase = 0;
+  auto slot_off = [&](int tt) __attribute__((always_inline)) -> uint32_t {
+    if constexpr (kRingTaps % NR == 0) return (uint32_t)((tt % NR) * kRingSlot);
+    else return (uint32_t)(((sbase + tt) % NR) * kRingSlot);
+  };
+
+  float16v accf[2][2];
+  int acci[FLUSH ? 2 : 1][2][16];
+  half8 fa[2][2], fb[2][2];  // [buffer][block]: fragments of one 16-code substep
+  int buf = 0;               // patch buffer of the current chunk
+
+  // first fragments of the stream
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm) fa[0][bm] = lds_frag(aaddr[bm][0]);
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) fb[0][bn] = lds_frag(baddr(bn, 0, 0));
+
+  for (;;) {
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          accf[bm][bn][r] = 0.0f;
+          if (FLUSH) acci[bm][bn][r] = 0;
+        }
+    const bool has_next = ntile < T;
+    int since = 0;
+    for (int c = 0; c < nch; ++c) {
+      const bool last_chunk = c + 1 == nch;
+      // the chunk after this one in the stream: its patch rows, channel chunk and weights
+      const int64_t nbase = last_chunk ? nxt.base : cur.base;
+      const int nc = last_chunk ? 0 : c + 1;
+      const int nm0 = last_chunk ? nxt.m0 : cur.m0;
+      const bool nlive = !last_chunk || has_next;
+      const int npx = nlive ? (last_chunk ? nxt.px : cur.px) : 0;  // 0: every lane reads zeros
+      const char* nsrc0 =
+          reinterpret_cast<const char*>(xg + nbase * a.W * a.Cp + (int64_t)nc * kKStep);
+      uint32_t bcur[2];
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn) bcur[bn] = baddr(bn, 0, buf);
+      static_for<0, kRingTaps>([&](auto tc) __attribute__((always_inline)) {
+        constexpr int t = decltype(tc)::value;
+        // (1) retire this wave's weight image of step s+1 (issued at step s-1; the only younger
+        // vector-memory op is the patch piece step s-1 issued after it, if any), then the
+        // barrier makes every wave's image visible and frees the slot of step s-1
+        // younger ops: the weight images of steps s+3-NR .. s-1 (2 instructions each) and
+        // the patch pieces of steps s+2-NR .. s-1 (issued after those steps' images)
+        constexpr int nyoung = [] {
+          int n = 2 * (NR - 3);
+          for (int j = 1; j <= NR - 2; ++j) n += ((t - j + 2 * kRingTaps) % kRingTaps) < PI;
+          return n;
+        }();
+        if constexpr (RING_AB != 1) TQ_WAIT_VM(nyoung);  // (RING_AB 1: timing only, no wait)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // (2) weight image of step s+NR-1 into the slot of step s-1; one patch piece of the
+        // next chunk
+        if constexpr (t + NR - 1 < kRingTaps)
+          issue_w(cur.m0, t + NR - 1, c, 0, true, slot_off(t + NR - 1));
+        else
+          issue_w(nm0, t + NR - 1 - kRingTaps, nc, 0, nlive, slot_off(t + NR - 1));
+        if constexpr (t < PI) issue_piece(t, nsrc0, npx, buf ^ 1);
+        // (3) B addresses of step s+1 (next tap, or tap 0 of the next chunk's buffer)
+        uint32_t bnx[2];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          bnx[bn] = t + 1 < kRingTaps ? baddr(bn, (t + 1) % kRingTaps, buf)
+                                      : baddr(bn, 0, buf ^ 1);
+        // (4) four substeps; the fragments of substep k+1 are read before substep k's MFMAs
+        const uint32_t soff = slot_off(t), nsoff = slot_off(t + 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cb = k & 1, nb = cb ^ 1;
+          // (at a tile's last step the k = 3 reads fetch the next tile's weights but this
+          // tile's pixels: they are read again after the epilogue)
+          if (k < 3) {
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm) fa[nb][bm] = lds_frag(aaddr[bm][k + 1] + soff);
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn) fb[nb][bn] = lds_frag(bcur[bn] + 32 * (k + 1));
+          } else {
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm) fa[nb][bm] = lds_frag(aaddr[bm][0] + nsoff);
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn) fb[nb][bn] = lds_frag(bnx[bn]);
+          }
+#pragma unroll
+          for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn)
+#if RING_AB == 2  // timing only: no MFMA (fragments kept live)
+              asm volatile("" ::"v"(fa[cb][bm]), "v"(fb[cb][bn]));
+#else
+              accf[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[cb][bm], fb[cb][bn],
+                                                                    accf[bm][bn], 0, 0, 0);
+#endif
+          // keep the order as written: the next substep's four reads, then this substep's four
+          // MFMAs (the scheduler otherwise recycles one fragment register: read, wait, MFMA)
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMAs
+        }
+        // after 4 substeps the next step's fragments sit in buffer 0 again
+        bcur[0] = bnx[0];
+        bcur[1] = bnx[1];
+        if (FLUSH && a.kc_chunk > 0 && t + 1 < kRingTaps && ++since == a.kc_chunk) {
+          since = 0;
+#pragma unroll
+          for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                acci[bm][bn][r] += (int)accf[bm][bn][r];
+                accf[bm][bn][r] = 0.0f;
+              }
+        }
+      });
+      // window end at every chunk end (chunk-major K order)
+      if (FLUSH) {
+        since = 0;
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              acci[bm][bn][r] += (int)accf[bm][bn][r];
+              accf[bm][bn][r] = 0.0f;
+            }
+      }
+      buf ^= 1;
+      sbase = (sbase + kRingTaps) % NR;
+    }
+
+    // ---- epilogue from the MFMA layout: lane (r32, hh) of block (bm, bn) holds channels
+    // m0 + wm + 32 bm + 8 q + 4 hh + [0, 4) of pixel column wn + 32 bn + r32
+    if constexpr (FAST) {
+      const int cl = cur.m0 + wm + 4 * hh;  // the lane's first channel
+      const double* cf = coef + 2 * cl;
+      static_for<0, 2>([&](auto bnc) __attribute__((always_inline)) {
+        constexpr int bn = decltype(bnc)::value;
+        const int j = wn + 32 * bn + r32;
+        const int64_t p = cur.p0 + j;
+        const bool okp = j < BNv && p < a.P;
+        const int64_t pc = okp ? p * a.Cout + cl : 0;
+        if (!okp || (RING_AB == 4 && a.out != (float*)p)) return;
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm) {
+          float4 rv[4];  // one block's residuals first: their latency overlaps the fold
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bool ok = a.residual && cl + 32 * bm + 8 * q < a.Cout;
+            rv[q] = ok ? *reinterpret_cast<const float4*>(a.residual + pc + 32 * bm + 8 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int d = 32 * bm + 8 * q;
+            if (cl + d >= a.Cout) continue;
+            const float4 r = rv[q];
+            const float rr[4] = {r.x, r.y, r.z, r.w};
+            float y[4], o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int acc = FLUSH ? acci[bm][bn][4 * q + e] : (int)accf[bm][bn][4 * q + e];
+              y[e] = fold_acc(acc, (coef_t)cf[2 * (d + e)], (coef_t)cf[2 * (d + e) + 1]) + rr[e];
+              o[e] = y[e] != y[e] ? y[e] : fmaxf(y[e], 0.0f);  // torch.relu keeps NaN
+              y[e] = fmaxf(y[e], 0.0f);                         // TR(NaN) = 0
+            }
+            if (a.out)
+              *reinterpret_cast<float4*>(a.out + pc + d) = make_float4(o[0], o[1], o[2], o[3]);
+            uint32_t qa[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) qa[e] = lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
+            *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d) =
+                make_uint2(qa[0] | (qa[1] << 16), qa[2] | (qa[3] << 16));
+            if (a.codes_b) {
+              uint32_t qb[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) qb[e] = lut_b[relu_q(y[e], a.inv_b, a.maxv_b)];
+              *reinterpret_cast<uint2*>(a.codes_b + p * a.cp_b + cl + d) =
+                  make_uint2(qb[0] | (qb[1] << 16), qb[2] | (qb[3] << 16));
+            }
+            if (cl + d + 4 == a.Cout) {  // the last quad zeroes the pad channels [Cout, cp)
+              if (a.cp_a > a.Cout)
+                *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d + 4) = make_uint2(0, 0);
+              if (a.codes_b && a.cp_b > a.Cout)
+                *reinterpret_cast<uint2*>(a.codes_b + p * a.cp_b + cl + d + 4) = make_uint2(0, 0);
+            }
+          }
+        }
+      });
+    } else {
+      static_for<0, 2>([&](auto bmc) __attribute__((always_inline)) {
+        constexpr int bm = decltype(bmc)::value;
+        float4 rv[2][4];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int co = cur.m0 + wm + 32 * bm + 8 * q + 4 * hh;
+            const int j = wn + 32 * bn + r32;
+            const int64_t p = cur.p0 + j;
+            const bool ok = a.residual && co < a.Cout && j < BNv && p < a.P;
+            rv[bn][q] = ok ? *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int co = cur.m0 + wm + 32 * bm + 8 * q + 4 * hh;
+            const int j = wn + 32 * bn + r32;
+            const int64_t p = cur.p0 + j;
+            if (co >= a.Cout || j >= BNv || p >= a.P) continue;
+            if (RING_AB == 4 && a.out != (float*)p) continue;  // timing only: no epilogue
+            int acc4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc4[e] = FLUSH ? acci[bm][bn][4 * q + e] : (int)accf[bm][bn][4 * q + e];
+            coef_t sc[4], sh[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              sc[e] = (coef_t)coef[2 * (co + e)];
+              sh[e] = (coef_t)coef[2 * (co + e) + 1];
+            }
+            emit4_nhwc_res(a, p, co, acc4, sc, sh, rv[bn][q], lut_a, lut_b);
+          }
+      });
+    }
+
+    if (!has_next) break;
+    // ---- next tile: its patch chunk 0 and weight steps 0/1 are already staged or in flight
+    tile = ntile;
+    cur = nxt;
+    ntile = tile + G;
+    nxt = ring_tile(a, ntile < T ? ntile : tile, R, mt, a.m_slow, ptc);
+    setup_b(cur);
+    // its first fragments (the last step of the previous tile did not prefetch across)
+    // are read after the barrier that retires step 1 -- step 0's image is already visible
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm) fa[0][bm] = lds_frag(aaddr[bm][0]);
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) fb[0][bn] = lds_frag(baddr(bn, 0, buf));
+  }
+}
+
+template <int PI, bool FLUSH, bool FAST>
+hipError_t launch_ring_fast(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
+                            hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv2d_tp_ring_kernel<PI, FLUSH, FAST>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  conv2d_tp_ring_kernel<PI, FLUSH, FAST>
+      <<<dim3((unsigned)grid), kRingThreads, lds, stream>>>(a, R, ptc);
+  return hipGetLastError();
+}
+
+// the FAST epilogue's form: ReLU, fp16 codes_a (+ codes_b) each served by a code table
+bool ring_fast_epilogue(const ConvArgs& a) {
+  return a.relu == 1 && a.codes_a != nullptr && a.lut_a > 0 && a.fmt_a == kCodesF16 &&
+         (a.codes_b == nullptr || (a.lut_b > 0 && a.fmt_b == kCodesF16));
+}
+
+template <int PI, bool FLUSH>
+hipError_t launch_ring_cfg(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
+                           hipStream_t stream) {
+  return ring_fast_epilogue(a) ? launch_ring_fast<PI, FLUSH, true>(a, R, ptc, grid, lds, stream)
+                               : launch_ring_fast<PI, FLUSH, false>(a, R, ptc, grid, lds, stream);
+}
+
+// Largest patch (pixels) over every tile: the row pattern repeats every Ho / gcd(R, Ho) tiles.
+int64_t ring_max_patch_px(const ConvArgs& a, int R) {
+  int64_t g = R, r = a.Ho;
+  while (r) {
+    const int64_t t = g % r;
+    g = r;
+    r = t;
+  }
+  const int64_t ptc = ((int64_t)a.N * a.Ho + R - 1) / R;
+  int64_t period = a.Ho / g;
+  if (period > ptc) period = ptc;
+  int64_t best = 0;
+  for (int64_t j = 0; j < period; ++j) {
+    const RingTile t = ring_tile(a, j, R, 1, 0, ptc);
+    if (t.px > best) best = t.px;
+  }
+  return best;
+}
+
+int ring_pieces(const ConvArgs& a, int R) {
+  const int64_t px = ring_max_patch_px(a, R);
+  for (int pi = 3; pi <= 6; ++pi)
+    if (px <= ring_pxs(pi)) return pi;
+  return -1;
+}
+
+int64_t ring_lds_bytes(const ConvArgs& a, int pi) {
+  return ring_coef_off(pi, ring_slots(pi)) + (int64_t)a.Cout * 16 + conv_lut_bytes(a);
+}
+
+}  // namespace
+
+bool conv_ring_eligible(const ConvArgs& a, int out_nhwc) {
+  if (!out_nhwc || a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1 || a.dh != 1 ||
+      a.dw != 1 || a.Cp % kKStep != 0 || a.Kp != 9 * a.Cp || (a.Cout & 3) != 0 ||
+      a.Wo > kRingBN || a.Wo < 1 || a.ds_x != nullptr || a.relu == kActSwish)
+    return false;
+  if (a.H != a.Ho || a.W != a.Wo) return false;  // "same" padding: stride 1, pad 1
+  const int R = kRingBN / a.Wo;
+  const int pi = ring_pieces(a, R);
+  return pi > 0 && ring_lds_bytes(a, pi) <= 160 * 1024;
+}
+
+hipError_t launch_conv2d_ring(const ConvArgs& a, hipStream_t stream) {
+  if (!conv_ring_eligible(a, 1)) return hipErrorInvalidValue;
+  const int R = kRingBN / a.Wo;
+  const int pi = ring_pieces(a, R);
+  const int64_t ptc = ((int64_t)a.N * a.Ho + R - 1) / R;
+  const int64_t tiles = ptc * ((a.Cout + kRingBM - 1) / kRingBM);
+  int64_t grid = device_cus();
+  const char* genv = getenv("TQ_RING_GRID");  // tests: fewer workgroups, more tiles each
+  if (genv && atoi(genv) > 0) grid = atoi(genv);
+  if (grid > tiles) grid = tiles;
+  const size_t lds = (size_t)ring_lds_bytes(a, pi);
+  const bool flush = a.kc_steps != 0;  // 0: the whole K range is one exact window
+  switch (pi) {
+    case 3: return flush ? launch_ring_cfg<3, true>(a, R, ptc, grid, lds, stream)
+                         : launch_ring_cfg<3, false>(a, R, ptc, grid, lds, stream);
+    case 4: return flush ? launch_ring_cfg<4, true>(a, R, ptc, grid, lds, stream)
+                         : launch_ring_cfg<4, false>(a, R, ptc, grid, lds, stream);
+    case 5: return flush ? launch_ring_cfg<5, true>(a, R, ptc, grid, lds, stream)
+                         : launch_ring_cfg<5, false>(a, R, ptc, grid, lds, stream);
+    default: return flush ? launch_ring_cfg<6, true>(a, R, ptc, grid, lds, stream)
+                          : launch_ring_cfg<6, false>(a, R, ptc, grid, lds, stream);
+  }
+}
+
+}  // namespace tq

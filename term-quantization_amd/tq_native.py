@@ -224,8 +224,9 @@ def version():
 
 
 def sync_faults():
-    """Bounded in-kernel waits (row-strip team syncs, LSTM step exchange) that ran out since
-    the last call (then cleared; synchronous): 0 in a healthy run (tq_sync_faults)."""
+    """Bounded in-kernel waits that ran out since the last call (then cleared; synchronous):
+    the row-strip conv engine's team syncs, the only bounded spin left (tq_sync_faults); 0 in
+    a healthy run."""
     n = ctypes.c_uint32(0)
     _check(lib().tq_sync_faults(ctypes.byref(n)))
     return int(n.value)
@@ -241,7 +242,8 @@ def lstm_seq_workspace_bytes(batch, hidden):
 
 
 def lstm_seq(gx, w_hh, b_hh, h0, c0, out, c_out):
-    """A whole LSTM layer's recurrence in one persistent launch (tq_lstm_seq_f32): gx
+    """A whole LSTM layer's recurrence from one call (tq_lstm_seq_f32: T launches of the fused
+    step kernel, h W_hh^T + gates + cell): gx
     [T, B, 4H], w_hh [4H, H], b_hh [4H] or None, h0/c0/c_out [B, H], out [T, B, H], contiguous
     fp32 CUDA tensors; the workspace is cached per (device, B, H)."""
     t, b, h4 = gx.shape

@@ -221,7 +221,30 @@ def test_module_path_teacher_forced_code_flips_are_midpoint_straddles(bench_mode
                     assert np.all(np.abs(v.astype(np.float64) - lo * sf) <= 8 * ulp + lo * sf *
                                   2.0 ** -22), r["name"]
             block_in = r2["out"]
+        print("BN-fold seam: %d of %d activation codes (module path vs fused executor, teacher "
+              "forced, 8 images) differ (%.2e), all one-step midpoint straddles"
+              % (flips, total, flips / max(total, 1)))
         assert total > 0 and flips <= total * 1e-4, (flips, total)
+
+
+def test_free_running_drift_from_module_path(bench_model):
+    """The measured path free-running: FusedResNet (what bench.py times) against the module
+    path (TRConv2dLayer + torch BN / ReLU / add: the reference composition) on the whole
+    256-image bench batch, with nothing teacher forced -- so the midpoint code flips of the
+    stem and BN-fold seams propagate through all 19 layers.  Records the top-1 agreement and
+    the logit deviation max |dlogit| / max |logit|."""
+    qmodel, x = bench_model
+    fused = tq_fuse.FusedResNet(qmodel)
+    with torch.no_grad():
+        lf = fused(x).double()
+        lm = qmodel(x).double()
+    torch.cuda.synchronize()
+    agree = float((lf.argmax(1) == lm.argmax(1)).double().mean())
+    dev = float((lf - lm).abs().max() / lm.abs().max())
+    mean_dev = float((lf - lm).abs().mean() / lm.abs().mean())
+    print("free-running drift (256 images): top-1 agreement %.4f, max |dlogit| / max |logit| "
+          "%.3e, mean |dlogit| / mean |logit| %.3e" % (agree, dev, mean_dev))
+    assert agree >= 0.95 and dev <= 5e-2, (agree, dev)
 
 
 def fused_next(rec, r):
