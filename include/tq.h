@@ -284,6 +284,25 @@ int tq_conv2d_termpair_wide(const int16_t *act_codes, int64_t n, int64_t h, int6
                             int32_t out_nhwc, void *stream);
 
 /*
+ * Squeeze-excite gate of an EfficientNet MBConv block (reference cnn_models/__init__.py:
+ * 52-65: both squeeze-excite convs term-revealed at (16, 1, 16)), one launch:
+ *   v   = TR(x_sq[n][c]; sf_r, bits_r, terms_r)            (int, as tq_act_encode)
+ *   y1  = fp32(double(sum_c v[c] w_r[j][c]) * scale_r + b_r[j])        j < cse
+ *   v2  = TR(y1 * sigmoid(y1); sf_e, bits_e, terms_e)                   (torch's fp32 swish)
+ *   y2  = fp32(double(sum_j v2[j] w_e_t[j][c]) * scale_e + b_e[c])      c < c
+ *   gate[n][c] = 1 / (1 + exp(-y2))                                     (torch's fp32 sigmoid)
+ * x_sq [n][c] fp32 (the block's pooled activations); w_r [cse][cpr] (cpr = roundup(c, 8),
+ * pad columns zero) and w_e_t [cse][c] (the expand conv's [c][cse] codes transposed) int32
+ * weight codes; b_r [cse],
+ * b_e [c] fp32 or NULL; scale_* = double(sf_x) * double(sf_w) of each conv; gate [n][c]
+ * fp32.  Sums are exact (int64); bits <= 14 activations, <= 16-bit weight codes.
+ */
+int tq_se_gate_f32(const float *x_sq, int64_t n, int64_t c, const int32_t *w_r, int64_t cse,
+                   double scale_r, const float *b_r, float sf_r, int32_t bits_r,
+                   int32_t terms_r, const int32_t *w_e_t, double scale_e, const float *b_e,
+                   float sf_e, int32_t bits_e, int32_t terms_e, float *gate, void *stream);
+
+/*
  * Depthwise term-pair conv with a fused epilogue (MobileNet-V2's dw conv -> BN -> ReLU6 and
  * the following project conv's input TR), channels_last:
  *   y = fp32(acc * ch_scale[c] + ch_shift[c])   (folded eval BatchNorm, fp64)

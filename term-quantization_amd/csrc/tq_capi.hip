@@ -163,6 +163,43 @@ int tq_act_encode_act(const float* x, int64_t n, int64_t c, int64_t h, int64_t w
                     "act_encode_act launch");
 }
 
+int tq_se_gate_f32(const float* x_sq, int64_t n, int64_t c, const int32_t* w_r, int64_t cse,
+                   double scale_r, const float* b_r, float sf_r, int32_t bits_r,
+                   int32_t terms_r, const int32_t* w_e_t, double scale_e, const float* b_e,
+                   float sf_e, int32_t bits_e, int32_t terms_e, float* gate, void* stream) {
+  if (n < 0 || c < 1 || cse < 1 || c > (1 << 20) || cse > (1 << 20))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "se_gate: bad shape");
+  if (n > 0 && (x_sq == nullptr || w_r == nullptr || w_e_t == nullptr || gate == nullptr))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "se_gate: null buffer");
+  if (bits_r < 0 || bits_r > 14 || bits_e < 0 || bits_e > 14)
+    return fail(TQ_ERR_UNSUPPORTED, "se_gate: activation bitwidths must be <= 14");
+  if (!(sf_r >= 0.0f) || !(sf_e >= 0.0f))
+    return fail(TQ_ERR_INVALID_ARGUMENT, "se_gate: sf must be >= 0");
+  const int64_t cpr = (c + 7) / 8 * 8;
+  if ((cpr + cse) * 4 > 64 * 1024)
+    return fail(TQ_ERR_UNSUPPORTED, "se_gate: channels too many for one workgroup's LDS");
+  tq::SeGateArgs a;
+  a.x_sq = x_sq;
+  a.N = (int)n;
+  a.C = (int)c;
+  a.w_r = w_r;
+  a.Cse = (int)cse;
+  a.Cpr = (int)cpr;
+  a.scale_r = scale_r;
+  a.bias_r = b_r;
+  a.inv_r = 1.0 / (double)sf_r;
+  a.maxv_r = (float)((1u << bits_r) - 1u);
+  a.k_r = terms_r < 0 ? 0 : terms_r;
+  a.w_e_t = w_e_t;
+  a.scale_e = scale_e;
+  a.bias_e = b_e;
+  a.inv_e = 1.0 / (double)sf_e;
+  a.maxv_e = (float)((1u << bits_e) - 1u);
+  a.k_e = terms_e < 0 ? 0 : terms_e;
+  a.gate = gate;
+  return hip_status(tq::launch_se_gate(a, (hipStream_t)stream), "se_gate launch");
+}
+
 int64_t tq_conv2d_cout_align(void) { return 128; }
 
 int32_t tq_conv2d_num_configs(void) { return tq::conv_num_configs(); }

@@ -136,6 +136,28 @@ struct PoolArgs {
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream);
 
+// Squeeze-excite gate (tq_se.hip): gate = sigmoid(expand(swish(reduce(x_sq)))), both 1x1
+// convs term-pair with int32 weight codes and int64 sums (as tr_conv_wide.hip).
+struct SeGateArgs {
+  const float* x_sq;      // [N][C] pooled activations
+  int N, C;
+  const int32_t* w_r;     // reduce conv weight codes [Cse][Cpr] (Cpr = roundup(C, 8), pad 0)
+  int Cse, Cpr;
+  double scale_r;         // double(fp32 sf_x) * double(fp32 sf_w)
+  const float* bias_r;    // [Cse] or nullptr
+  double inv_r;           // RN64(1 / sf) of the reduce conv's input quantizer
+  float maxv_r;
+  int k_r;
+  const int32_t* w_e_t;   // expand conv weight codes transposed, [Cse][C]
+  double scale_e;
+  const float* bias_e;    // [C] or nullptr
+  double inv_e;
+  float maxv_e;
+  int k_e;
+  float* gate;            // [N][C]
+};
+hipError_t launch_se_gate(const SeGateArgs& a, hipStream_t stream);
+
 hipError_t launch_act_encode_act(const float* x, const float* ch_scale, const float* ch_shift,
                                  const float* gate, int act, float* out,
                                  int64_t N, int64_t C, int64_t H, int64_t W, float sf,

@@ -426,7 +426,14 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
     const float* __restrict__ ch_shift, const float* __restrict__ gate, int act,
     float* __restrict__ out,
     int16_t* __restrict__ codes, int64_t npix, int64_t HW, int C, int Cp, double inv_sf,
-    float maxv, int k, int fmt) {
+    float maxv, int k, int fmt, int lut_n) {
+  // the code table (lut_n = maxv + 1 entries, 0 = none): TR of a value costs its a1
+  // rounding and one LDS read (tq_device.h lut_codes; signed values after swish / a gate too)
+  extern __shared__ __attribute__((aligned(16))) uint16_t lut[];
+  if (lut_n) {
+    lut_build(lut, lut_n, k, fmt, threadIdx.x, 256);
+    __syncthreads();
+  }
   const int chunks = Cp / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= npix * chunks) return;
@@ -478,7 +485,11 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
     for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? gate[img * C + c0 + i] * v[i] : 0.0f;
   }
   uint32_t b[8];
-  if (act_nonneg(act) && !gate && inv_sf > 0.0 && inv_sf <= 1.0e308) {
+  if (lut_n) {
+    lut_codes<8>(v, inv_sf, maxv, fmt, act_nonneg(act) && !gate, lut, b);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = c0 + i < C ? b[i] : 0u;
+  } else if (act_nonneg(act) && !gate && inv_sf > 0.0 && inv_sf <= 1.0e308) {
     // ReLU / ReLU6: v >= 0 and never NaN -- the epilogues' sign-free fast path (same codes)
     const int npeel = relu_peels(maxv, k);
 #pragma unroll
@@ -508,9 +519,13 @@ hipError_t launch_act_encode_act(const float* x, const float* ch_scale, const fl
   const int64_t npix = N * H * W;
   const int64_t n = npix * (Cp / 8);
   if (n == 0) return hipSuccess;
-  act_encode_act_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
-      x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp,
-      1.0 / (double)sf, maxv, k, fmt);
+  const double inv = 1.0 / (double)sf;
+  const char* lut_env = getenv("TQ_LUT");  // 0: computed codes (tests, A/B; read per launch)
+  const int lut_n = (!(lut_env && atoi(lut_env) == 0) && inv > 0.0 && inv <= 1.0e308 &&
+                     (int)maxv + 1 <= kLutMax) ? (int)maxv + 1 : 0;
+  act_encode_act_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, (size_t)lut_n * 2, stream>>>(
+      x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, inv, maxv, k,
+      fmt, lut_n);
   return hipGetLastError();
 }
 

@@ -511,9 +511,12 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
     return launch_conv2d_direct(a, 1, stream);
   }
-  // tap-ring engine: config 13, or TQ_RING=1 (read per launch: tests switch it)
+  // tap-ring engine: config 13, and the default for the 3x3 stride-1 convs with Cout >= 128
+  // (ResNet-18 layer2/3/4: 1.1-1.5x the direct / input-patch engines, tools/gpu_ring_probe.sh);
+  // TQ_RING=0 / 1 forces it off / on (read per launch: tests switch it)
   const char* ring = getenv("TQ_RING");
-  if ((cfg == 12 || (cfg < 0 && ring && atoi(ring) == 1)) && conv_ring_eligible(a, out_nhwc))
+  const bool ring_on = ring ? atoi(ring) == 1 : a.Cout >= 128;
+  if ((cfg == 12 || (cfg < 0 && ring_on)) && conv_ring_eligible(a, out_nhwc))
     return launch_conv2d_ring(a, stream);
   if (cfg == 12) cfg = -1;
   static const char* strip = getenv("TQ_STRIP");  // A/B override (tools only): 0 off

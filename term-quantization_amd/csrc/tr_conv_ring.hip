@@ -50,26 +50,41 @@ namespace tq {
 
 namespace {
 
-constexpr int kRingThreads = 512;
 constexpr int kRingBM = 128;            // Cout rows per tile
-constexpr int kRingBN = 256;            // pixel columns per tile
-constexpr int kRingSlot = kRingBM * 128;  // bytes per ring slot
-constexpr int kPitch = 144;             // patch bytes per pixel
 constexpr int kRingTaps = 9;            // 3 x 3
+constexpr int kRingExtra = 160 + 8192 + 2048;  // zero pixel + Cout <= 512 coefficients + tables
 
-__host__ __device__ constexpr int ring_pbuf(int pi) { return 8 * pi * 1024; }
-__host__ __device__ constexpr int ring_pxs(int pi) { return ring_pbuf(pi) / kPitch; }
-__host__ __device__ constexpr int ring_patch_off(int nr) { return nr * kRingSlot; }
-__host__ __device__ constexpr int ring_zero_off(int pi, int nr) {
-  return ring_patch_off(nr) + 2 * ring_pbuf(pi);
-}
-__host__ __device__ constexpr int ring_coef_off(int pi, int nr) {
-  return ring_zero_off(pi, nr) + 160;
-}
-// Weight ring depth for a patch of PI pieces per wave: as deep as the 160 KB of LDS allows
-// (3 x 16 KB beside two 48 KB patch buffers ... 6 beside two 24 KB ones).  The barrier of
-// step s retires step s+1's image, issued at step s+2-NR: NR-2 steps of DMA lead.
-__host__ __device__ constexpr int ring_slots(int pi) { return pi >= 6 ? 3 : pi == 5 ? 4 : pi == 4 ? 5 : 6; }
+// Two shapes of the engine:
+//   NW = 8, KS = 64: one 512-thread workgroup per CU (160 KB of LDS), tile 128 x 256, K-steps
+//                    of 64 codes (one 64-channel chunk of one tap);
+//   NW = 4, KS = 32: two 256-thread workgroups per CU (80 KB of LDS each), tile 128 x 128,
+//                    K-steps of 32 codes: one workgroup's epilogue, barrier waits and chunk
+//                    switches run beside the other's MFMAs.
+// Wave tile 64 x 64 either way (2 x 2 blocks of 32 x 32).
+template <int NW, int KS>
+struct RingGeom {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BN = 64 * (NW / 2);   // pixel columns per tile
+  static constexpr int ROWB = KS * 2;        // bytes per weight row and K-step
+  static constexpr int CH = ROWB / 16;       // 16-byte chunks per row (8 or 4)
+  static constexpr int SH = CH == 8 ? 1 : 2; // row swizzle shift: chunk ^= (row >> SH) & (CH-1)
+  static constexpr int SLOT = kRingBM * ROWB;
+  static constexpr int WI = SLOT / 1024 / NW;  // weight DMA instructions per wave and step
+  static constexpr int PITCH = ROWB + 16;      // patch bytes per pixel (odd number of 16 B)
+  static constexpr int SUB = KS / 16;          // MFMA substeps per K-step
+  static constexpr int BUDGET = NW == 8 ? 160 * 1024 : 80 * 1024;
+  static constexpr int pbuf(int pi) { return NW * pi * 1024; }
+  static constexpr int pxs(int pi) { return pbuf(pi) / PITCH; }
+  // weight ring depth: as deep as the LDS budget allows beside two patch buffers.  The
+  // barrier of step s retires step s+1's image, issued at step s+2-NR: NR-2 steps of lead.
+  static constexpr int slots(int pi) {
+    const int n = (BUDGET - 2 * pbuf(pi) - kRingExtra) / SLOT;
+    return n > 6 ? 6 : n;
+  }
+  static constexpr int patch_off(int nr) { return nr * SLOT; }
+  static constexpr int zero_off(int pi, int nr) { return patch_off(nr) + 2 * pbuf(pi); }
+  static constexpr int coef_off(int pi, int nr) { return zero_off(pi, nr) + 160; }
+};
 
 // The rows of one tile and the input rows its patch holds.
 struct RingTile {
@@ -116,7 +131,7 @@ struct ic {
   static constexpr int value = V;
 };
 template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
+__host__ __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
     f(ic<I>{});
     static_for<I + 1, N>(f);
@@ -124,6 +139,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 __device__ __forceinline__ half8 lds_frag(uint32_t byte_addr) {
+  if (RING_AB == 7) return (half8)(_Float16)(byte_addr & 7);  // timing only: no LDS reads
   return __builtin_bit_cast(
       half8, *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(
                  (uintptr_t)byte_addr));
@@ -132,20 +148,24 @@ __device__ __forceinline__ half8 lds_frag(uint32_t byte_addr) {
 // FAST: the fused ResNet executor's epilogue form, specialised at launch -- ReLU, fp16 codes
 // from the code tables (every code output has one), Cout % 4 == 0 -- with per-pixel base
 // pointers and compile-time channel offsets; other forms run the shared emit4_nhwc_res.
-template <int PI, bool FLUSH, bool FAST>
-__global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArgs a, int R,
-                                                                        int64_t ptc) {
-  constexpr int NR = ring_slots(PI);
+template <int NW, int KS, int PI, bool FLUSH, bool FAST>
+__global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, int R,
+                                                                   int64_t ptc) {
+  using Gm = RingGeom<NW, KS>;
+  constexpr int NR = Gm::slots(PI);
+  constexpr int WI = Gm::WI, CH = Gm::CH, SH = Gm::SH, SUB = Gm::SUB;
+  constexpr int kRingSlot = Gm::SLOT, kPitch = Gm::PITCH;
+  static_assert(NR >= 3, "the LDS budget must hold three weight images");
   // the next chunk's last patch piece (tap PI-1) must be older than the weight image the
   // barrier of that chunk's last step retires (issued at tap 10-NR)
   static_assert(PI <= 10 - NR, "patch pieces must land before the chunk switch");
   extern __shared__ __attribute__((aligned(16))) u32x4 ring_lds[];
   const uint32_t lds0 =
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)ring_lds;
-  constexpr uint32_t kPatchOff = ring_patch_off(NR);
-  constexpr uint32_t kZeroOff = ring_zero_off(PI, NR);
+  constexpr uint32_t kPatchOff = Gm::patch_off(NR);
+  constexpr uint32_t kZeroOff = Gm::zero_off(PI, NR);
   double* coef = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(ring_lds) +
-                                           ring_coef_off(PI, NR));
+                                           Gm::coef_off(PI, NR));
   uint16_t *lut_a, *lut_b;
   conv_luts(a, reinterpret_cast<uint16_t*>(coef + 2 * a.Cout), lut_a, lut_b);
 
@@ -154,21 +174,21 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31;
   const int hh = lane >> 5;
-  const int wm = (wave >> 2) * 64;  // this wave's Cout rows [wm, wm + 64) of the tile
-  const int wn = (wave & 3) * 64;   // and pixel columns [wn, wn + 64)
+  const int wm = (wave / (NW / 2)) * 64;  // this wave's Cout rows [wm, wm + 64) of the tile
+  const int wn = (wave % (NW / 2)) * 64;  // and pixel columns [wn, wn + 64)
   const int mt = (a.Cout + kRingBM - 1) / kRingBM;
   const int64_t T = ptc * mt;
   const int64_t G = gridDim.x;
   const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
   const int BNv = R * a.Wo;
-  const int nch = a.Cp / kKStep;
+  const int nch = a.Cp / KS;
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
   const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
   const char* __restrict__ wgb = reinterpret_cast<const char*>(a.w);
   const char* zsrc = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
 
   // epilogue coefficients of every channel, the zero pixel
-  for (int i = tid; i < a.Cout; i += kRingThreads) {
+  for (int i = tid; i < a.Cout; i += Gm::THREADS) {
     coef[2 * i] = a.ch_scale ? a.ch_scale[i] : a.scale;
     coef[2 * i + 1] = a.ch_scale ? a.ch_shift[i] : (a.bias ? (double)a.bias[i] : 0.0);
   }
@@ -176,21 +196,21 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
     *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(ring_lds) + kZeroOff + tid * 16) =
         (u32x4)0u;
 
-  // ---- weight DMA: wave w moves rows [16 w, 16 w + 16) of a slot in 2 instructions of 8 rows
-  int64_t wlane[2];  // per-lane byte offset of its 16-byte source chunk within a K column
-  uint32_t wdst[2];  // LDS byte offset of the instruction within a slot
+  // ---- weight DMA: wave w moves WI instructions of 1024 / ROWB rows each of every slot
+  int64_t wlane[WI];  // per-lane byte offset of its 16-byte source chunk within a K column
+  uint32_t wdst[WI];  // LDS byte offset of the instruction within a slot
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = (wave * 2 + i) * 8 + (lane >> 3);
-    wlane[i] = (int64_t)r * a.Kp * 2 + (((lane & 7) ^ ((r >> 1) & 7)) * 16);
-    wdst[i] = (uint32_t)((wave * 2 + i) * 1024);
+  for (int i = 0; i < WI; ++i) {
+    const int r = (wave * WI + i) * (1024 / Gm::ROWB) + lane / CH;
+    wlane[i] = (int64_t)r * a.Kp * 2 + (((lane % CH) ^ ((r >> SH) & (CH - 1))) * 16);
+    wdst[i] = (uint32_t)((wave * WI + i) * 1024);
   }
   // weight image of K-step (tap t, chunk c) of the tile whose first row is m0 into `slot`
   auto issue_w = [&](int m0, int t, int c, int slot, bool live, uint32_t soff = 0)
       __attribute__((always_inline)) {
-    const int64_t col = ((int64_t)m0 * a.Kp + (int64_t)t * a.Cp + (int64_t)c * kKStep) * 2;
+    const int64_t col = ((int64_t)m0 * a.Kp + (int64_t)t * a.Cp + (int64_t)c * KS) * 2;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WI; ++i)
       ring_dma(live ? wgb + col + wlane[i] : zsrc, lds0 + slot * kRingSlot + soff + wdst[i]);
   };
 
@@ -204,14 +224,14 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
   for (int j = 0; j < PI; ++j) {
     const int b = (wave * PI + j) * 1024 + lane * 16;
     const int q = b / kPitch, ch = (b - q * kPitch) >> 4;
-    ppix[j] = ch < 8 ? q : 1 << 20;
+    ppix[j] = ch < CH ? q : 1 << 20;
     poff[j] = (uint32_t)((q * a.Cp + ch * 8) * 2);
   }
   // src0: byte address of the chunk's first patch pixel, channel chunk c (uniform)
   auto issue_piece = [&](int j, const char* src0, int px, int buf)
       __attribute__((always_inline)) {
     const char* src = ppix[j] < px ? src0 + poff[j] : zsrc;
-    ring_dma(src, lds0 + kPatchOff + buf * ring_pbuf(PI) + (wave * PI + j) * 1024);
+    ring_dma(src, lds0 + kPatchOff + buf * Gm::pbuf(PI) + (wave * PI + j) * 1024);
   };
 
   // ---- B fragment pixels of the current tile: patch pixel of tap (0, 0) and in-bounds taps
@@ -241,21 +261,26 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
   };
   // LDS byte address of B block bn's substep-0 fragment at tap t of the patch in buffer buf
   auto baddr = [&](int bn, int t, int buf) __attribute__((always_inline)) {
-    const uint32_t in = lds0 + kPatchOff + buf * ring_pbuf(PI) +
+    const uint32_t in = lds0 + kPatchOff + buf * Gm::pbuf(PI) +
                         (uint32_t)(pix[bn] + (t / 3) * a.W + (t % 3)) * kPitch + hh * 16;
     const uint32_t zero = lds0 + kZeroOff + hh * 16;
     return ((tmask[bn] >> t) & 1u) ? in : zero;
   };
   // A fragment byte address (slot 0) of block bm, substep k: swizzled row image
-  uint32_t aaddr[2][4];
+  uint32_t aaddr[2][SUB];
 #pragma unroll
   for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < SUB; ++k) {
       const int row = wm + 32 * bm + r32;
-      aaddr[bm][k] = lds0 + (uint32_t)(row * 128 + (((2 * k + hh) ^ ((row >> 1) & 7)) * 16));
+      aaddr[bm][k] = lds0 + (uint32_t)(row * Gm::ROWB +
+                                       (((2 * k + hh) ^ ((row >> SH) & (CH - 1))) * 16));
     }
 
+#if RING_AB == 8  // timing only: odd workgroups start ~half a tile late (epilogue stagger)
+  if (blockIdx.x & 1)
+    for (int i = 0; i < a.ab; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   // ---- the tile stream
   int64_t tile = g;
   RingTile cur = ring_tile(a, tile, R, mt, a.m_slow, ptc);
@@ -309,7 +334,7 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
       const bool nlive = !last_chunk || has_next;
       const int npx = nlive ? (last_chunk ? nxt.px : cur.px) : 0;  // 0: every lane reads zeros
       const char* nsrc0 =
-          reinterpret_cast<const char*>(xg + nbase * a.W * a.Cp + (int64_t)nc * kKStep);
+          reinterpret_cast<const char*>(xg + nbase * a.W * a.Cp + (int64_t)nc * KS);
       uint32_t bcur[2];
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn) bcur[bn] = baddr(bn, 0, buf);
@@ -321,12 +346,12 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
         // younger ops: the weight images of steps s+3-NR .. s-1 (2 instructions each) and
         // the patch pieces of steps s+2-NR .. s-1 (issued after those steps' images)
         constexpr int nyoung = [] {
-          int n = 2 * (NR - 3);
+          int n = WI * (NR - 3);
           for (int j = 1; j <= NR - 2; ++j) n += ((t - j + 2 * kRingTaps) % kRingTaps) < PI;
           return n;
         }();
         if constexpr (RING_AB != 1) TQ_WAIT_VM(nyoung);  // (RING_AB 1: timing only, no wait)
-        __builtin_amdgcn_s_barrier();
+        if constexpr (RING_AB != 5) __builtin_amdgcn_s_barrier();  // (5: timing only)
         asm volatile("" ::: "memory");
         // (2) weight image of step s+NR-1 into the slot of step s-1; one patch piece of the
         // next chunk
@@ -341,14 +366,14 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
         for (int bn = 0; bn < 2; ++bn)
           bnx[bn] = t + 1 < kRingTaps ? baddr(bn, (t + 1) % kRingTaps, buf)
                                       : baddr(bn, 0, buf ^ 1);
-        // (4) four substeps; the fragments of substep k+1 are read before substep k's MFMAs
+        // (4) SUB substeps; the fragments of substep k+1 are read before substep k's MFMAs
         const uint32_t soff = slot_off(t), nsoff = slot_off(t + 1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < SUB; ++k) {
           const int cb = k & 1, nb = cb ^ 1;
           // (at a tile's last step the k = 3 reads fetch the next tile's weights but this
           // tile's pixels: they are read again after the epilogue)
-          if (k < 3) {
+          if (k + 1 < SUB) {
 #pragma unroll
             for (int bm = 0; bm < 2; ++bm) fa[nb][bm] = lds_frag(aaddr[bm][k + 1] + soff);
 #pragma unroll
@@ -374,10 +399,11 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
           __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS reads
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMAs
         }
-        // after 4 substeps the next step's fragments sit in buffer 0 again
+        // after SUB (even) substeps the next step's fragments sit in buffer 0 again
         bcur[0] = bnx[0];
         bcur[1] = bnx[1];
-        if (FLUSH && a.kc_chunk > 0 && t + 1 < kRingTaps && ++since == a.kc_chunk) {
+        if (FLUSH && RING_AB != 6 && a.kc_chunk > 0 && t + 1 < kRingTaps &&
+            ++since == a.kc_chunk) {  // (RING_AB 6: timing only, chunk-end windows)
           since = 0;
 #pragma unroll
           for (int bm = 0; bm < 2; ++bm)
@@ -412,27 +438,30 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
     if constexpr (FAST) {
       const int cl = cur.m0 + wm + 4 * hh;  // the lane's first channel
       const double* cf = coef + 2 * cl;
+      // one pixel block's residual loads first (2 round trips per tile instead of 4)
       static_for<0, 2>([&](auto bnc) __attribute__((always_inline)) {
         constexpr int bn = decltype(bnc)::value;
         const int j = wn + 32 * bn + r32;
         const int64_t p = cur.p0 + j;
         const bool okp = j < BNv && p < a.P;
         const int64_t pc = okp ? p * a.Cout + cl : 0;
+        float4 rv[2][4];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bool ok = RING_AB != 10 && a.residual && okp && cl + 32 * bm + 8 * q < a.Cout;
+            rv[bm][q] = ok ? *reinterpret_cast<const float4*>(a.residual + pc + 32 * bm + 8 * q)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
         if (!okp || (RING_AB == 4 && a.out != (float*)p)) return;
 #pragma unroll
         for (int bm = 0; bm < 2; ++bm) {
-          float4 rv[4];  // one block's residuals first: their latency overlaps the fold
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const bool ok = a.residual && cl + 32 * bm + 8 * q < a.Cout;
-            rv[q] = ok ? *reinterpret_cast<const float4*>(a.residual + pc + 32 * bm + 8 * q)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int d = 32 * bm + 8 * q;
             if (cl + d >= a.Cout) continue;
-            const float4 r = rv[q];
+            const float4 r = rv[bm][q];
             const float rr[4] = {r.x, r.y, r.z, r.w};
             float y[4], o[4];
 #pragma unroll
@@ -442,11 +471,21 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
               o[e] = y[e] != y[e] ? y[e] : fmaxf(y[e], 0.0f);  // torch.relu keeps NaN
               y[e] = fmaxf(y[e], 0.0f);                         // TR(NaN) = 0
             }
+            if (RING_AB == 9) {  // timing only: no stores (values kept live)
+              asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+              uint32_t qz[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) qz[e] = lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
+              asm volatile("" ::"v"(qz[0]), "v"(qz[1]), "v"(qz[2]), "v"(qz[3]));
+              continue;
+            }
             if (a.out)
               *reinterpret_cast<float4*>(a.out + pc + d) = make_float4(o[0], o[1], o[2], o[3]);
             uint32_t qa[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) qa[e] = lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
+            for (int e = 0; e < 4; ++e)
+              qa[e] = RING_AB == 11 ? relu_q(y[e], a.inv_a, a.maxv_a)
+                                    : lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
             *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d) =
                 make_uint2(qa[0] | (qa[1] << 16), qa[2] | (qa[3] << 16));
             if (a.codes_b) {
@@ -511,28 +550,30 @@ __global__ __launch_bounds__(kRingThreads, 2) void conv2d_tp_ring_kernel(ConvArg
     ntile = tile + G;
     nxt = ring_tile(a, ntile < T ? ntile : tile, R, mt, a.m_slow, ptc);
     setup_b(cur);
-    // its first fragments (the last step of the previous tile did not prefetch across)
-    // are read after the barrier that retires step 1 -- step 0's image is already visible
+    // its first fragments (the last step of the previous tile prefetched this tile's
+    // weights but the old pixels): step 0's image and patch were retired by the barrier of
+    // the previous tile's last step.  Its ring slot is the stream's step index mod NR, which
+    // is not 0 when 9 * nch is not a multiple of NR.
 #pragma unroll
-    for (int bm = 0; bm < 2; ++bm) fa[0][bm] = lds_frag(aaddr[bm][0]);
+    for (int bm = 0; bm < 2; ++bm) fa[0][bm] = lds_frag(aaddr[bm][0] + slot_off(0));
 #pragma unroll
     for (int bn = 0; bn < 2; ++bn) fb[0][bn] = lds_frag(baddr(bn, 0, buf));
   }
 }
 
-template <int PI, bool FLUSH, bool FAST>
+template <int NW, int KS, int PI, bool FLUSH, bool FAST>
 hipError_t launch_ring_fast(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
                             hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv2d_tp_ring_kernel<PI, FLUSH, FAST>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        reinterpret_cast<const void*>(&conv2d_tp_ring_kernel<NW, KS, PI, FLUSH, FAST>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, RingGeom<NW, KS>::BUDGET);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  conv2d_tp_ring_kernel<PI, FLUSH, FAST>
-      <<<dim3((unsigned)grid), kRingThreads, lds, stream>>>(a, R, ptc);
+  conv2d_tp_ring_kernel<NW, KS, PI, FLUSH, FAST>
+      <<<dim3((unsigned)grid), 64 * NW, lds, stream>>>(a, R, ptc);
   return hipGetLastError();
 }
 
@@ -542,11 +583,16 @@ bool ring_fast_epilogue(const ConvArgs& a) {
          (a.codes_b == nullptr || (a.lut_b > 0 && a.fmt_b == kCodesF16));
 }
 
-template <int PI, bool FLUSH>
-hipError_t launch_ring_cfg(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
-                           hipStream_t stream) {
-  return ring_fast_epilogue(a) ? launch_ring_fast<PI, FLUSH, true>(a, R, ptc, grid, lds, stream)
-                               : launch_ring_fast<PI, FLUSH, false>(a, R, ptc, grid, lds, stream);
+template <int NW, int KS, int PI>
+hipError_t launch_ring_pi(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
+                          hipStream_t stream) {
+  const bool flush = a.kc_steps != 0;  // 0: the whole K range is one exact window
+  const bool fast = ring_fast_epilogue(a);
+  if (flush)
+    return fast ? launch_ring_fast<NW, KS, PI, true, true>(a, R, ptc, grid, lds, stream)
+                : launch_ring_fast<NW, KS, PI, true, false>(a, R, ptc, grid, lds, stream);
+  return fast ? launch_ring_fast<NW, KS, PI, false, true>(a, R, ptc, grid, lds, stream)
+              : launch_ring_fast<NW, KS, PI, false, false>(a, R, ptc, grid, lds, stream);
 }
 
 // Largest patch (pixels) over every tile: the row pattern repeats every Ho / gcd(R, Ho) tiles.
@@ -568,52 +614,78 @@ int64_t ring_max_patch_px(const ConvArgs& a, int R) {
   return best;
 }
 
-int ring_pieces(const ConvArgs& a, int R) {
-  const int64_t px = ring_max_patch_px(a, R);
-  for (int pi = 3; pi <= 6; ++pi)
-    if (px <= ring_pxs(pi)) return pi;
-  return -1;
+// A launch plan of one engine shape: rows per tile, patch pieces per wave, dynamic LDS.
+struct RingPlan {
+  int R, pi;
+  int64_t lds;
+};
+
+template <int NW, int KS>
+bool ring_plan(const ConvArgs& a, RingPlan* pl) {
+  using Gm = RingGeom<NW, KS>;
+  if (a.Cp % KS != 0 || a.Wo > Gm::BN) return false;
+  pl->R = Gm::BN / a.Wo;
+  const int64_t px = ring_max_patch_px(a, pl->R);
+  for (int pi = 3; pi <= 6; ++pi) {
+    const int nr = Gm::slots(pi);
+    if (nr < 3 || pi > 10 - nr || px > Gm::pxs(pi)) continue;
+    pl->pi = pi;
+    pl->lds = Gm::coef_off(pi, nr) + (int64_t)a.Cout * 16 + conv_lut_bytes(a);
+    return pl->lds <= Gm::BUDGET;
+  }
+  return false;
 }
 
-int64_t ring_lds_bytes(const ConvArgs& a, int pi) {
-  return ring_coef_off(pi, ring_slots(pi)) + (int64_t)a.Cout * 16 + conv_lut_bytes(a);
+template <int NW, int KS>
+hipError_t launch_ring_shape(const ConvArgs& a, const RingPlan& pl, int per_cu,
+                             hipStream_t stream) {
+  const int64_t ptc = ((int64_t)a.N * a.Ho + pl.R - 1) / pl.R;
+  const int64_t tiles = ptc * ((a.Cout + kRingBM - 1) / kRingBM);
+  int64_t grid = (int64_t)per_cu * device_cus();
+  const char* genv = getenv("TQ_RING_GRID");  // tests: fewer workgroups, more tiles each
+  if (genv && atoi(genv) > 0) grid = atoi(genv);
+  if (grid > tiles) grid = tiles;
+  const size_t lds = (size_t)pl.lds;
+  hipError_t e = hipErrorInvalidValue;
+  static_for<3, 7>([&](auto pc) {
+    constexpr int PI = decltype(pc)::value;
+    constexpr int NR = RingGeom<NW, KS>::slots(PI);
+    if constexpr (NR >= 3 && PI <= 10 - NR)  // the shapes ring_plan can choose
+      if (pl.pi == PI) e = launch_ring_pi<NW, KS, PI>(a, pl.R, ptc, grid, lds, stream);
+  });
+  return e;
+}
+
+// TQ_RING_V=1: the 8-wave shape, 2: the two-workgroups-per-CU shape (read per launch)
+int ring_shape() {
+  const char* v = getenv("TQ_RING_V");
+  return v && atoi(v) == 2 ? 2 : 1;
+}
+
+bool ring_common(const ConvArgs& a, int out_nhwc) {
+  return out_nhwc && a.KH == 3 && a.KW == 3 && a.sh == 1 && a.sw == 1 && a.dh == 1 &&
+         a.dw == 1 && a.Kp == 9 * a.Cp && (a.Cout & 3) == 0 && a.Wo >= 1 &&
+         a.ds_x == nullptr && a.relu != kActSwish && a.Cout <= 512 &&
+         a.H == a.Ho && a.W == a.Wo;  // "same" padding: stride 1, pad 1
 }
 
 }  // namespace
 
 bool conv_ring_eligible(const ConvArgs& a, int out_nhwc) {
-  if (!out_nhwc || a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1 || a.dh != 1 ||
-      a.dw != 1 || a.Cp % kKStep != 0 || a.Kp != 9 * a.Cp || (a.Cout & 3) != 0 ||
-      a.Wo > kRingBN || a.Wo < 1 || a.ds_x != nullptr || a.relu == kActSwish)
-    return false;
-  if (a.H != a.Ho || a.W != a.Wo) return false;  // "same" padding: stride 1, pad 1
-  const int R = kRingBN / a.Wo;
-  const int pi = ring_pieces(a, R);
-  return pi > 0 && ring_lds_bytes(a, pi) <= 160 * 1024;
+  RingPlan pl;
+  if (!ring_common(a, out_nhwc)) return false;
+  return ring_shape() == 2 ? ring_plan<4, 32>(a, &pl) : ring_plan<8, 64>(a, &pl);
 }
 
 hipError_t launch_conv2d_ring(const ConvArgs& a, hipStream_t stream) {
-  if (!conv_ring_eligible(a, 1)) return hipErrorInvalidValue;
-  const int R = kRingBN / a.Wo;
-  const int pi = ring_pieces(a, R);
-  const int64_t ptc = ((int64_t)a.N * a.Ho + R - 1) / R;
-  const int64_t tiles = ptc * ((a.Cout + kRingBM - 1) / kRingBM);
-  int64_t grid = device_cus();
-  const char* genv = getenv("TQ_RING_GRID");  // tests: fewer workgroups, more tiles each
-  if (genv && atoi(genv) > 0) grid = atoi(genv);
-  if (grid > tiles) grid = tiles;
-  const size_t lds = (size_t)ring_lds_bytes(a, pi);
-  const bool flush = a.kc_steps != 0;  // 0: the whole K range is one exact window
-  switch (pi) {
-    case 3: return flush ? launch_ring_cfg<3, true>(a, R, ptc, grid, lds, stream)
-                         : launch_ring_cfg<3, false>(a, R, ptc, grid, lds, stream);
-    case 4: return flush ? launch_ring_cfg<4, true>(a, R, ptc, grid, lds, stream)
-                         : launch_ring_cfg<4, false>(a, R, ptc, grid, lds, stream);
-    case 5: return flush ? launch_ring_cfg<5, true>(a, R, ptc, grid, lds, stream)
-                         : launch_ring_cfg<5, false>(a, R, ptc, grid, lds, stream);
-    default: return flush ? launch_ring_cfg<6, true>(a, R, ptc, grid, lds, stream)
-                          : launch_ring_cfg<6, false>(a, R, ptc, grid, lds, stream);
+  RingPlan pl;
+  if (!ring_common(a, 1)) return hipErrorInvalidValue;
+  if (ring_shape() == 2) {
+    if (!ring_plan<4, 32>(a, &pl)) return hipErrorInvalidValue;
+    return launch_ring_shape<4, 32>(a, pl, 2, stream);
   }
+  if (!ring_plan<8, 64>(a, &pl)) return hipErrorInvalidValue;
+  return launch_ring_shape<8, 64>(a, pl, 1, stream);
 }
 
 }  // namespace tq

@@ -560,6 +560,36 @@ class FusedMobileNetV2(nn.Module):
 # "wide" kernel) and the pooling stay module calls: a few KB per image.
 
 
+def _se_plan(block):
+    """tq_native.se_gate arguments of an MBConv block's squeeze-excite convs, or None when
+    they are not the calibrated 1x1 "wide" TRConv2dLayers the fused kernel covers."""
+    convs = (getattr(block, "_se_reduce", None), getattr(block, "_se_expand", None))
+    for m in convs:
+        if not isinstance(m, tr_layer.TRConv2dLayer) or getattr(m, "mode", None) != "wide":
+            return None
+        c = m.conv
+        if (c.kernel_size != (1, 1) or c.stride != (1, 1) or c.groups != 1 or
+                any(tq_ops.static_padding(c)) or c.padding != (0, 0) or
+                m.input_quant.tracking or m.data_bits > 14):
+            return None
+    r, e = convs
+    cse, cin = r.conv.out_channels, r.conv.in_channels
+    if e.conv.in_channels != cse or e.conv.out_channels != cin:
+        return None
+    if tuple(r.w_codes.shape) != (cse, tq_ops.act_channels(cin)) or \
+            tuple(e.w_codes.shape) != (cin, tq_ops.act_channels(cse)):
+        return None
+
+    def conv_args(m, w):
+        scale = float(np.float32(m.input_quant.sf)) * float(np.float32(m.w_sf))
+        bias = m.conv.bias.detach().float().contiguous() if m.conv.bias is not None else None
+        quant = (m.input_quant.sf, m.data_bits, m.data_terms)
+        return w, scale, bias, quant
+    # the expand conv's codes k-major ([Cse][C]): the kernel's lanes run along C
+    w_e_t = e.w_codes[:, :cse].t().contiguous()
+    return {"cse": cse, "args": conv_args(r, r.w_codes.contiguous()) + conv_args(e, w_e_t)}
+
+
 def _conv_out_static(conv, h, w):
     top, bottom, left, right = tq_ops.static_padding(conv.conv)
     c = conv.conv
@@ -585,15 +615,25 @@ class _MBConv(object):
         self.project = _Conv(block._project_conv, block._bn2, nonneg=False)
         self.use_res = (block.id_skip and block.stride == 1 and
                         block.input_filters == block.output_filters)
+        self.se = _se_plan(block) if self.has_se else None
 
     def first_consumer(self):
         return self.expand if self.expand is not None else self.dw.consumer
 
     def gate(self, d):
-        """sigmoid(se_expand(swish(se_reduce(avgpool(d))))) as fp32 [N, C] (module calls:
-        the squeeze-excite convs are TRConv2dLayers, efficientnet_pytorch's composition)."""
+        """sigmoid(se_expand(swish(se_reduce(avgpool(d))))) as fp32 [N, C]: torch's pooling,
+        then the fused squeeze-excite kernel (tq_se_gate_f32: both term-pair convs, swish and
+        sigmoid in one launch, bit-identical to the module calls) when the block's convs are
+        the "wide" TRConv2dLayers it covers (TQ_SE_FUSED=0: the module calls)."""
         b = self.block
         x_sq = nn.functional.adaptive_avg_pool2d(d, 1)
+        if self.se is not None and os.environ.get("TQ_SE_FUSED", "1") != "0":
+            n, c = d.shape[0], d.shape[1]
+            g = torch.empty((n, c), dtype=torch.float32, device=d.device)
+            tq_ops._launch("se_gate", n * c * 2 * self.se["cse"],
+                           lambda: tq_native.se_gate(x_sq.reshape(n, c).contiguous(),
+                                                     *self.se["args"], g))
+            return g
         x_sq = b._se_expand(b._swish(b._se_reduce(x_sq)))
         return torch.sigmoid(x_sq).reshape(d.shape[0], d.shape[1]).contiguous()
 

@@ -46,6 +46,8 @@ _SIGNATURES = {
                           _i32, _vp, _i64, _i32, _vp],
     "tq_act_encode": [_vp, _i32, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _i64, _i32,
                       _vp],
+    "tq_se_gate_f32": [_vp, _i64, _i64, _vp, _i64, _f64, _vp, _f32, _i32, _i32, _vp, _f64, _vp,
+                       _f32, _i32, _i32, _vp, _vp],
     "tq_conv2d_cout_align": [],
     "tq_conv2d_num_configs": [],
     "tq_conv2d_workspace_bytes": [_i64, _i64],
@@ -337,6 +339,25 @@ def act_encode_act(x, sf, bitwidth, num_keep_terms, codes, act=None, gate=None, 
                                      code_format(codes), _stream(x))
     _check(rc)
     return codes
+
+
+def se_gate(x_sq, w_r, scale_r, b_r, quant_r, w_e_t, scale_e, b_e, quant_e, gate):
+    """EfficientNet squeeze-excite gate in one launch (tq_se_gate_f32): gate [N, C] =
+    sigmoid(expand(swish(reduce(x_sq)))) with x_sq fp32 [N, C], int32 weight codes w_r
+    [Cse, roundup(C, 8)] and w_e_t [Cse, C] (the expand conv's codes transposed), quant_* =
+    (sf, bits, terms) of each conv's input quantizer, scale_* = double(sf_x) * double(sf_w)."""
+    n, c = x_sq.shape
+    cse = w_r.shape[0]
+    for t, shp in ((w_r, (cse, (c + 7) // 8 * 8)), (w_e_t, (cse, c))):
+        if t.dtype != torch.int32 or tuple(t.shape) != shp or not t.is_contiguous():
+            raise RuntimeError("se_gate: weight codes must be contiguous int32 %s" % (shp,))
+    with torch.cuda.device(x_sq.device):
+        rc = lib().tq_se_gate_f32(_ptr(x_sq), n, c, _ptr(w_r), cse, float(scale_r), _ptr(b_r),
+                                  float(quant_r[0]), int(quant_r[1]), int(quant_r[2]), _ptr(w_e_t),
+                                  float(scale_e), _ptr(b_e), float(quant_e[0]),
+                                  int(quant_e[1]), int(quant_e[2]), _ptr(gate), _stream(x_sq))
+    _check(rc)
+    return gate
 
 
 def conv2d_cout_align():

@@ -392,3 +392,38 @@ def test_fused_resnet_downsample_phase(monkeypatch):
         assert not downs[0].conv2.fusable_downsample(downs[0].down)
         two = fused(x)
     assert torch.equal(one, two)
+
+
+@pytest.mark.parametrize("act", [None, 6, "swish"])
+@pytest.mark.parametrize("gated", [False, True])
+@pytest.mark.parametrize("fmt", [torch.int16, torch.float16])
+def test_act_encode_act_code_table_bit_identical(act, gated, fmt, monkeypatch):
+    """tq_act_encode_act's code table (tq_device.h lut_codes: ReLU6 values and, with swish, a
+    gate or no activation, signed ones) against its computed codes (TQ_LUT=0) and against the
+    oracle's TR of the activated value: bit-identical codes, with negative, zero, NaN and
+    infinite inputs and a channel count that leaves pad channels."""
+    n, c, hw = 3, 44, 9
+    torch.manual_seed(7)
+    x = (torch.randn(n, c, hw, hw, device=DEV) * 3).contiguous(memory_format=torch.channels_last)
+    flat = x.permute(0, 2, 3, 1).view(-1)  # the NHWC storage
+    flat[::89] = float("nan")
+    flat[1::97] = float("inf")
+    flat[2::101] = -float("inf")
+    flat[3::103] = -0.0
+    gate = torch.rand(n, c, device=DEV) if gated else None
+    cp = 48
+    res = []
+    for lut in ("1", "0"):
+        monkeypatch.setenv("TQ_LUT", lut)
+        codes = torch.full((n, hw, hw, cp), 77, dtype=fmt, device=DEV)
+        out = torch.empty_like(x)
+        tq_native.act_encode_act(x, 0.05, 9, 3, codes, act=act, gate=gate, out=out)
+        res.append((codes.float().cpu(), out.cpu()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1].view(torch.int32), res[1][1].view(torch.int32))
+    v = res[0][1].permute(0, 2, 3, 1).contiguous()
+    if gated:
+        v = v * gate.cpu()[:, None, None, :]
+    ref = torch.from_numpy(oracle.tr(v.numpy(), 0.05, 9, 1, 3)) / 0.05
+    assert torch.equal(res[0][0][..., :c], ref.round())
+    assert (res[0][0][..., c:] == 0).all()

@@ -186,3 +186,32 @@ def test_swish_is_torchs_fp32_swish_bit_for_bit():
                    0.01, 9, 1, 3)
     exp = np.rint(yq.reshape(4, 17, 9, 64) / np.float32(0.01)).astype(np.int64)
     assert np.array_equal(codes.long().cpu().numpy(), exp)
+
+
+def test_fused_se_gate_bit_identical_to_module_path(net, monkeypatch):
+    """The fused squeeze-excite kernel (tq_se_gate_f32) against the module calls it replaces
+    (TRConv2dLayer "wide" reduce / expand convs, torch swish and sigmoid) on every SE block's
+    real depthwise output: the gates must be bit-identical (exact int64 term sums, one fp64
+    fold each, torch's fp32 swish / sigmoid compositions)."""
+    import torch.nn.functional as F
+    q, x = net
+    fused = tq_fuse.FusedEfficientNet(q)
+    with torch.no_grad():
+        cap = []
+        fused(x, capture=cap)
+        checked = 0
+        for i, b in enumerate(fused.blocks):
+            if not b.has_se:
+                continue
+            assert b.se is not None, i  # every b0 SE block takes the fused kernel
+            rec = next(r for r in cap if r["name"] == "block%d.dw" % i)
+            d, g = rec["out"], rec["gate"]
+            blk = b.block
+            ref = torch.sigmoid(blk._se_expand(blk._swish(blk._se_reduce(
+                F.adaptive_avg_pool2d(d, 1))))).reshape(d.shape[0], d.shape[1])
+            assert torch.equal(g.view(torch.int32), ref.contiguous().view(torch.int32)), i
+            monkeypatch.setenv("TQ_SE_FUSED", "0")
+            assert torch.equal(b.gate(d), g), i
+            monkeypatch.delenv("TQ_SE_FUSED")
+            checked += 1
+    assert checked == 16

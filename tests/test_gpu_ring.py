@@ -20,6 +20,14 @@ DEV = "cuda:0"
 RING = 13  # MFMA config number of the tap-ring engine
 
 
+@pytest.fixture(autouse=True, params=["1", "2"])
+def shape(request, monkeypatch):
+    """Both engine shapes: 1 = one 8-wave workgroup per CU (128 x 256 tiles, 64-code K-steps),
+    2 = two 4-wave workgroups per CU (128 x 128 tiles, 32-code K-steps)."""
+    monkeypatch.setenv("TQ_RING_V", request.param)
+    return request.param
+
+
 def _run(codes, lay, cout, hw, *, cfg, sc, sh, res=None, relu=True, out=True, codes_b=False,
          fmt=torch.float16, kc_steps=0, kc_chunk=-1):
     n = codes.shape[0]
@@ -71,9 +79,10 @@ def _layers(conv, x, monkeypatch):
     (256, 256, 14, 6),    # layer 3: two Cout tiles per pixel tile
     (512, 512, 7, 9),     # layer 4: 36-row tiles over 5 images
     (64, 64, 56, 2),      # layer 1 shape (one chunk, half-empty Cout tile)
-    (192, 132, 9, 3),     # three chunks, partial Cout tile, R = 28
+    (192, 132, 9, 3),     # three chunks, partial Cout tile, R = 28; with one workgroup
+                          # its second tile starts at ring slot 27 mod NR != 0
 ])
-@pytest.mark.parametrize("grid", ["0", "3"])
+@pytest.mark.parametrize("grid", ["0", "3", "1"])
 def test_ring_bit_identical_to_valu(cin, cout, hw, batch, grid, monkeypatch):
     conv, x, sc, sh, res = _case(cin, cout, hw, batch, seed=cin + cout + hw)
     lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
@@ -111,6 +120,7 @@ def test_ring_m_slow_order(monkeypatch):
     lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
     ref = _run(cv, lay_v, 512, 7, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16)
     monkeypatch.setenv("TQ_RING_GRID", "4")
+    monkeypatch.setenv("TQ_MSLOW", "1")
     got = _run(cm, lay_m, 512, 7, cfg=RING, sc=sc, sh=sh, res=res, kc_steps=lay_m.kc_steps,
                kc_chunk=lay_m.kc_chunk)
     assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
