@@ -196,9 +196,10 @@ void conv2d_tp_patch_kernel(
     // Exactness windows.  This kernel walks K chunk-major (taps inner); the host bounds every
     // window of kc_chunk CONSECUTIVE taps of one 64-code chunk (ConvArgs.kc_chunk), and the
     // fp32 sums are also flushed at the end of every chunk and of the piece, so each fp32
-    // window lies inside one bounded window.
-    const bool flushing = a.kc_chunk > 0;
-    const int kc_steps = flushing ? a.kc_chunk : (1 << 30);
+    // window lies inside one bounded window.  kc_chunk == 0 with kc_steps > 0 means a whole
+    // chunk fits one window but the full K does not: chunk-end flushes only.
+    const bool flushing = a.kc_chunk > 0 || a.kc_steps > 0;
+    const int kc_steps = a.kc_chunk > 0 ? a.kc_chunk : (1 << 30);
     int since_flush = 0;
 
     // Counted retirement: `issued` counts this wave's LDS-DMA instructions; mark[j] is its
