@@ -23,6 +23,7 @@ namespace tq {
 namespace {
 
 constexpr int kSeThreads = 256;
+constexpr int kSeU = 8;  // weight loads in flight per lane
 
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 #pragma unroll
@@ -43,8 +44,16 @@ __global__ __launch_bounds__(kSeThreads) void se_gate_kernel(SeGateArgs a) {
   // reduce conv: output j by wave j % 4, its lanes along the input channels
   for (int j = wave; j < a.Cse; j += kSeThreads / 64) {
     const int32_t* w = a.w_r + (int64_t)j * a.Cpr;
+    // kSeU independent loads in flight per lane (the loop is paced by L2 latency)
     int64_t acc = 0;
-    for (int c = lane; c < a.Cpr; c += 64) acc += (int64_t)vx[c] * (int64_t)w[c];
+    for (int c0 = lane; c0 < a.Cpr; c0 += 64 * kSeU) {
+      int32_t wv[kSeU];
+#pragma unroll
+      for (int u = 0; u < kSeU; ++u) wv[u] = c0 + 64 * u < a.Cpr ? w[c0 + 64 * u] : 0;
+#pragma unroll
+      for (int u = 0; u < kSeU; ++u)
+        if (c0 + 64 * u < a.Cpr) acc += (int64_t)vx[c0 + 64 * u] * (int64_t)wv[u];
+    }
     acc = wave_sum_i64(acc);
     if (lane == 0) {
       const float y = (float)((double)acc * a.scale_r + (a.bias_r ? (double)a.bias_r[j] : 0.0));
@@ -56,8 +65,15 @@ __global__ __launch_bounds__(kSeThreads) void se_gate_kernel(SeGateArgs a) {
   float* g = a.gate + (int64_t)n * a.C;
   for (int c = tid; c < a.C; c += kSeThreads) {
     int64_t acc = 0;
-    for (int j = 0; j < a.Cse; ++j)
-      acc += (int64_t)v2[j] * (int64_t)a.w_e_t[(int64_t)j * a.C + c];
+    for (int j0 = 0; j0 < a.Cse; j0 += kSeU) {
+      int32_t wv[kSeU];
+#pragma unroll
+      for (int u = 0; u < kSeU; ++u)
+        wv[u] = j0 + u < a.Cse ? a.w_e_t[(int64_t)(j0 + u) * a.C + c] : 0;
+#pragma unroll
+      for (int u = 0; u < kSeU; ++u)
+        if (j0 + u < a.Cse) acc += (int64_t)v2[j0 + u] * (int64_t)wv[u];
+    }
     const float y = (float)((double)acc * a.scale_e + (a.bias_e ? (double)a.bias_e[c] : 0.0));
     g[c] = 1.0f / (1.0f + expf(-y));
   }
