@@ -421,6 +421,10 @@ __global__ __launch_bounds__(256) void act_encode_kernel(const float* __restrict
 // one lane per 8 channels of a pixel): v = act(x) (none or swish, act_apply), out = v (if
 // out: the fp32 activation), v = fp32(gate[img][c] * v) (if gate: MBConvBlock.forward's
 // x = sigmoid(x_sq) * x), codes[p][c] = TR(v) for the next conv (pad channels zero).
+// Grid-stride: a few workgroups per CU, each building the code table once and then walking
+// many chunks (a table per 2048 values cost as much as the values); IDX is the index type
+// (uint32_t when npix * Cp / 8 and npix * C fit: no 64-bit divisions per chunk).
+template <typename IDX>
 __global__ __launch_bounds__(256) void act_encode_act_kernel(
     const float* __restrict__ x, const float* __restrict__ ch_scale,
     const float* __restrict__ ch_shift, const float* __restrict__ gate, int act,
@@ -434,78 +438,89 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
     lut_build(lut, lut_n, k, fmt, threadIdx.x, 256);
     __syncthreads();
   }
-  const int chunks = Cp / 8;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= npix * chunks) return;
-  const int64_t pix = t / chunks;
-  const int c0 = (int)(t - pix * chunks) * 8;
-  const int64_t img = pix / HW;
-  float v[8];
-  const bool vec = c0 + 8 <= C && (C & 3) == 0;
-  if (vec) {
-    const float4 x0 = *reinterpret_cast<const float4*>(x + pix * C + c0);
-    const float4 x1 = *reinterpret_cast<const float4*>(x + pix * C + c0 + 4);
-    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? x[pix * C + c0 + i] : 0.0f;
-  }
-  if (ch_scale) {  // eval BatchNorm as a per-channel fp32 affine (a stem's bn before its act)
-    if (vec) {  // 16-byte coefficient loads (4 per lane instead of 16 scalar ones)
-      const float4 s0 = *reinterpret_cast<const float4*>(ch_scale + c0);
-      const float4 s1 = *reinterpret_cast<const float4*>(ch_scale + c0 + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(ch_shift + c0);
-      const float4 h1 = *reinterpret_cast<const float4*>(ch_shift + c0 + 4);
-      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        v[i] = c0 + i < C ? fmaf(v[i], ch_scale[c0 + i], ch_shift[c0 + i]) : 0.0f;
-    }
-  }
-  float o[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) act_apply(act, v[i], o[i]);
-  if (out) {
+  const IDX chunks = (IDX)(Cp / 8);
+  const IDX total = (IDX)npix * chunks;
+  const IDX hw = (IDX)HW;
+  for (IDX t = (IDX)blockIdx.x * 256 + threadIdx.x; t < total; t += (IDX)gridDim.x * 256) {
+    const IDX pix = t / chunks;
+    const int c0 = (int)(t - pix * chunks) * 8;
+    const IDX img = pix / hw;
+    float v[8];
+    const bool vec = c0 + 8 <= C && (C & 3) == 0;
     if (vec) {
-      *reinterpret_cast<float4*>(out + pix * C + c0) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(out + pix * C + c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      const float4 x0 = *reinterpret_cast<const float4*>(x + pix * C + c0);
+      const float4 x1 = *reinterpret_cast<const float4*>(x + pix * C + c0 + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+      v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
     } else {
-#pragma unroll
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? x[pix * C + c0 + i] : 0.0f;
+    }
+    if (ch_scale) {  // eval BatchNorm as a per-channel fp32 affine (a stem's bn before its act)
+      if (vec) {  // 16-byte coefficient loads (4 per lane instead of 16 scalar ones)
+        const float4 s0 = *reinterpret_cast<const float4*>(ch_scale + c0);
+        const float4 s1 = *reinterpret_cast<const float4*>(ch_scale + c0 + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(ch_shift + c0);
+        const float4 h1 = *reinterpret_cast<const float4*>(ch_shift + c0 + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  #pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
+      } else {
+  #pragma unroll
+        for (int i = 0; i < 8; ++i)
+          v[i] = c0 + i < C ? fmaf(v[i], ch_scale[c0 + i], ch_shift[c0 + i]) : 0.0f;
+      }
+    }
+    float o[8];
+  #pragma unroll
+    for (int i = 0; i < 8; ++i) act_apply(act, v[i], o[i]);
+    if (out) {
+      if (vec) {
+        *reinterpret_cast<float4*>(out + pix * C + c0) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(out + pix * C + c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+  #pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + i < C) out[pix * C + c0 + i] = o[i];
+      }
+    }
+    if (gate) {
+      if (vec) {
+        const float4 g0 = *reinterpret_cast<const float4*>(gate + img * C + c0);
+        const float4 g1 = *reinterpret_cast<const float4*>(gate + img * C + c0 + 4);
+        const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+  #pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = g[i] * v[i];
+      } else {
+  #pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? gate[img * C + c0 + i] * v[i] : 0.0f;
+      }
+    }
+    uint32_t b[8];
+    if (lut_n) {
+      lut_codes<8>(v, inv_sf, maxv, fmt, act_nonneg(act) && !gate, lut, b);
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = c0 + i < C ? b[i] : 0u;
+    } else if (act_nonneg(act) && !gate && inv_sf > 0.0 && inv_sf <= 1.0e308) {
+      // ReLU / ReLU6: v >= 0 and never NaN -- the epilogues' sign-free fast path (same codes)
+      const int npeel = relu_peels(maxv, k);
+  #pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int32_t t4[4];
+        tr_values_relu4(v + 4 * h, inv_sf, maxv, npeel, t4);
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) b[4 * h + i] = c0 + 4 * h + i < C ? code_bits(t4[i], fmt) : 0u;
+      }
+    } else {
+  #pragma unroll
       for (int i = 0; i < 8; ++i)
-        if (c0 + i < C) out[pix * C + c0 + i] = o[i];
+        b[i] = c0 + i < C ? code_bits(tr_value_g1_inv(v[i], inv_sf, maxv, k), fmt) : 0u;
     }
+    *reinterpret_cast<uint4*>(codes + (int64_t)pix * Cp + c0) =
+        make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16),
+                   b[6] | (b[7] << 16));
   }
-  if (gate) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = c0 + i < C ? gate[img * C + c0 + i] * v[i] : 0.0f;
-  }
-  uint32_t b[8];
-  if (lut_n) {
-    lut_codes<8>(v, inv_sf, maxv, fmt, act_nonneg(act) && !gate, lut, b);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = c0 + i < C ? b[i] : 0u;
-  } else if (act_nonneg(act) && !gate && inv_sf > 0.0 && inv_sf <= 1.0e308) {
-    // ReLU / ReLU6: v >= 0 and never NaN -- the epilogues' sign-free fast path (same codes)
-    const int npeel = relu_peels(maxv, k);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int32_t t4[4];
-      tr_values_relu4(v + 4 * h, inv_sf, maxv, npeel, t4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) b[4 * h + i] = c0 + 4 * h + i < C ? code_bits(t4[i], fmt) : 0u;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      b[i] = c0 + i < C ? code_bits(tr_value_g1_inv(v[i], inv_sf, maxv, k), fmt) : 0u;
-  }
-  *reinterpret_cast<uint4*>(codes + pix * Cp + c0) =
-      make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
 }
 
 }  // namespace
@@ -523,9 +538,16 @@ hipError_t launch_act_encode_act(const float* x, const float* ch_scale, const fl
   const char* lut_env = getenv("TQ_LUT");  // 0: computed codes (tests, A/B; read per launch)
   const int lut_n = (!(lut_env && atoi(lut_env) == 0) && inv > 0.0 && inv <= 1.0e308 &&
                      (int)maxv + 1 <= kLutMax) ? (int)maxv + 1 : 0;
-  act_encode_act_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, (size_t)lut_n * 2, stream>>>(
-      x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, inv, maxv, k,
-      fmt, lut_n);
+  const int64_t grid = std::min<int64_t>((n + 255) / 256, (int64_t)device_cus() * 8);
+  const bool small = n < (1ll << 31) && npix * Cp < (1ll << 31);
+  if (small)
+    act_encode_act_kernel<uint32_t><<<dim3((unsigned)grid), 256, (size_t)lut_n * 2, stream>>>(
+        x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, inv, maxv,
+        k, fmt, lut_n);
+  else
+    act_encode_act_kernel<int64_t><<<dim3((unsigned)grid), 256, (size_t)lut_n * 2, stream>>>(
+        x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, inv, maxv,
+        k, fmt, lut_n);
   return hipGetLastError();
 }
 
