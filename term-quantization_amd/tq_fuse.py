@@ -376,6 +376,37 @@ class FusedResNet(nn.Module):
 # kernels touch HBM -- fp32 tensors only where a residual or the pooling needs them.
 
 
+def _run_chunks(streams, codes, xin, y, body):
+    """Run body(codes, xin, y) generators over image chunks of a batch, one chunk per HIP
+    stream, one launch per stream in turn (FusedResNet.forward_streams): every launch is
+    per-image independent, so the chunks compute exactly what one launch over the batch
+    does.  ``y`` (the head conv's output) is written chunk by chunk in place."""
+    cur = torch.cuda.current_stream(codes.device)
+    n = len(streams)
+    parts = [codes.chunk(n), xin.chunk(n) if xin is not None else [None] * n, y.chunk(n)]
+    gens = []
+    for s, c, xi, yi in zip(streams, *parts):
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            gens.append(body(c, xi, yi))
+    live = list(range(len(gens)))
+    while live:
+        nxt = []
+        for j in live:
+            with torch.cuda.stream(streams[j]):
+                if next(gens[j], StopIteration) is not StopIteration:
+                    nxt.append(j)
+        live = nxt
+    capturing = torch.cuda.is_current_stream_capturing()
+    for s, c, xi in zip(streams, parts[0], parts[1]):
+        cur.wait_stream(s)
+        if not capturing:  # (a captured graph keeps its private pool alive)
+            c.record_stream(s)
+            if xi is not None:
+                xi.record_stream(s)
+            y.record_stream(s)
+
+
 class _Codes(object):
     """What a producing epilogue needs to know about a consuming TR layer."""
 
@@ -457,6 +488,9 @@ class _InvRes(object):
         """The consumer of this block's input codes: the expand conv, else the dw conv."""
         return self.expand if self.expand is not None else self.dw.consumer
 
+    def out_hw(self, h, w):
+        return self.dw.out_hw(h, w)  # (the 1x1 convs keep the size)
+
 
 class FusedMobileNetV2(nn.Module):
     """Inference executor over a converted + calibrated MobileNet-V2 (cnn_models.mobilenet_v2
@@ -486,7 +520,36 @@ class FusedMobileNetV2(nn.Module):
         """Logits of a batch.  ``capture`` (a list, tests only) receives one record per
         term-pair / depthwise layer: {"name", "kind", "conv", "codes_in", "residual", "out",
         "codes_out"}; capture mode also stores every fp32 output."""
-        m = self.qmodel
+        codes, xin = self._stem(x, capture)
+        y = self._head_out(codes)
+        for _ in self._body(codes, xin, y, capture):
+            pass
+        return self._classify(y)
+
+    @torch.no_grad()
+    def forward_streams(self, x, streams):
+        """forward() with the blocks of len(streams) image chunks on their own HIP streams,
+        launched layer by layer round-robin (as FusedResNet.forward_streams): one chunk's
+        short launches fill the CUs the other's leave idle.  The torch stem conv and the
+        classifier run on the whole batch (their library kernels may pick another algorithm
+        for another batch size), so the logits are bit-identical to forward()'s."""
+        codes, xin = self._stem(x, None)
+        y = self._head_out(codes)
+        _run_chunks(streams, codes, xin, y, self._body)
+        return self._classify(y)
+
+    def _head_out(self, codes):
+        n, h, w, _ = codes.shape
+        for b in self.blocks:
+            h, w = b.out_hw(h, w)
+        return torch.empty((n, self.last.cout, h, w), dtype=torch.float32, device=codes.device,
+                           memory_format=torch.channels_last)
+
+    def _classify(self, y):
+        y = nn.functional.adaptive_avg_pool2d(y, 1).reshape(y.shape[0], -1)
+        return self.qmodel.classifier(y)
+
+    def _stem(self, x, capture):
         keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
         first = self.blocks[0].first_consumer()
@@ -507,13 +570,18 @@ class FusedMobileNetV2(nn.Module):
         if keep:
             capture.append({"name": "stem", "kind": "stem", "out": y0, "codes_out": codes,
                             "quant": first.quant})
-        xin = y0
+        return codes, y0
+
+    def _body(self, codes, xin, y, capture=None):
+        """The blocks and the last conv (into ``y``) as a generator: yields after each
+        launch."""
+        keep = capture is not None
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
-            c_in = codes
             if b.expand is not None:
                 h, hcodes, _ = b.expand(codes, out=True if keep else None, relu=6,
                                         next_a=b.dw.consumer)
+                yield
                 if keep:
                     capture.append({"name": "block%d.expand" % i, "kind": "conv",
                                     "conv": b.expand, "codes_in": codes, "residual": None,
@@ -521,6 +589,7 @@ class FusedMobileNetV2(nn.Module):
             else:
                 hcodes = codes
             d, pcodes = b.dw(hcodes, b.project, out=keep)
+            yield
             if keep:
                 capture.append({"name": "block%d.dw" % i, "kind": "dw", "conv": b.dw,
                                 "codes_in": hcodes, "residual": None, "out": d,
@@ -530,19 +599,19 @@ class FusedMobileNetV2(nn.Module):
             xout, codes, _ = b.project(pcodes, out=True if need_out else None,
                                        residual=xin if b.use_res else None, relu=False,
                                        next_a=consumer)
+            yield
             if keep:
                 capture.append({"name": "block%d.project" % i, "kind": "conv",
                                 "conv": b.project, "codes_in": pcodes,
                                 "residual": xin if b.use_res else None, "out": xout,
                                 "codes_out": codes, "relu": 0})
             xin = xout
-        y, _, _ = self.last(codes, out=True, relu=6)
+        self.last(codes, out=y, relu=6)
+        yield
         if keep:
             capture.append({"name": "last", "kind": "conv", "conv": self.last,
                             "codes_in": codes, "residual": None, "out": y, "codes_out": None,
                             "relu": 6})
-        y = nn.functional.adaptive_avg_pool2d(y, 1).reshape(y.shape[0], -1)
-        return m.classifier(y)
 
 
 # ---------------------------------------------------------------------------------------
@@ -620,6 +689,9 @@ class _MBConv(object):
     def first_consumer(self):
         return self.expand if self.expand is not None else self.dw.consumer
 
+    def out_hw(self, h, w):
+        return self.dw.out_hw(h, w)  # (the 1x1 convs keep the size)
+
     def gate(self, d):
         """sigmoid(se_expand(swish(se_reduce(avgpool(d))))) as fp32 [N, C]: torch's pooling,
         then the fused squeeze-excite kernel (tq_se_gate_f32: both term-pair convs, swish and
@@ -660,6 +732,34 @@ class FusedEfficientNet(nn.Module):
         """Logits of a batch.  ``capture`` (a list, tests only) receives one record per
         term-pair / depthwise layer: {"name", "kind", "conv", "codes_in", "residual", "out",
         "codes_out", "act", "gate"}; capture mode also stores every fp32 output."""
+        codes, xin = self._stem(x, capture)
+        y = self._head_out(codes)
+        for _ in self._body(codes, xin, y, capture):
+            pass
+        return self._classify(y)
+
+    @torch.no_grad()
+    def forward_streams(self, x, streams):
+        """forward() with the blocks of len(streams) image chunks on their own HIP streams
+        (FusedMobileNetV2.forward_streams); bit-identical logits."""
+        codes, xin = self._stem(x, None)
+        y = self._head_out(codes)
+        _run_chunks(streams, codes, xin, y, self._body)
+        return self._classify(y)
+
+    def _head_out(self, codes):
+        n, h, w, _ = codes.shape
+        for b in self.blocks:
+            h, w = b.out_hw(h, w)
+        return torch.empty((n, self.head.cout, h, w), dtype=torch.float32, device=codes.device,
+                           memory_format=torch.channels_last)
+
+    def _classify(self, y):
+        m = self.qmodel
+        y = m._avg_pooling(m._swish(y)).flatten(start_dim=1)
+        return m._fc(m._dropout(y))
+
+    def _stem(self, x, capture):
         m = self.qmodel
         keep = capture is not None
         x = x.contiguous(memory_format=torch.channels_last)
@@ -683,7 +783,12 @@ class FusedEfficientNet(nn.Module):
         if keep:
             capture.append({"name": "stem", "kind": "stem", "out": y0, "codes_out": codes,
                             "quant": first.quant})
-        xin = y0
+        return codes, y0
+
+    def _body(self, codes, xin, y, capture=None):
+        """The blocks and the head conv (into ``y``) as a generator: yields after each
+        launch."""
+        keep = capture is not None
         for i, b in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             if b.expand is not None:
@@ -691,6 +796,7 @@ class FusedEfficientNet(nn.Module):
                 # instantiation: 1x1 convs)
                 h, hcodes, _ = b.expand(codes, out=True if keep else None, relu="swish",
                                         next_a=b.dw.consumer)
+                yield
                 if keep:
                     capture.append({"name": "block%d.expand" % i, "kind": "conv",
                                     "conv": b.expand, "codes_in": codes, "residual": None,
@@ -699,15 +805,19 @@ class FusedEfficientNet(nn.Module):
                 hcodes = codes
             if b.has_se:
                 d, _ = b.dw(hcodes, None, out=True, act="swish")
+                yield
                 g = b.gate(d)
+                yield
                 pcodes = torch.empty((d.shape[0], d.shape[2], d.shape[3], b.project.cp_in),
-                                     dtype=b.project.code_dtype, device=x.device)
+                                     dtype=b.project.code_dtype, device=d.device)
                 tq_ops._launch("act_encode_act", 6 * d.numel(),
                                lambda: tq_native.act_encode_act(d, *b.project.quant, pcodes,
                                                                 gate=g))
+                yield
             else:
                 d, pcodes = b.dw(hcodes, b.project, out=keep, act="swish")
                 g = None
+                yield
             if keep:
                 capture.append({"name": "block%d.dw" % i, "kind": "dw", "conv": b.dw,
                                 "codes_in": hcodes, "residual": None, "out": d,
@@ -717,16 +827,16 @@ class FusedEfficientNet(nn.Module):
             xout, codes, _ = b.project(pcodes, out=True if need_out else None,
                                        residual=xin if b.use_res else None, relu=False,
                                        next_a=consumer)
+            yield
             if keep:
                 capture.append({"name": "block%d.project" % i, "kind": "conv",
                                 "conv": b.project, "codes_in": pcodes,
                                 "residual": xin if b.use_res else None, "out": xout,
                                 "codes_out": codes, "act": None})
             xin = xout
-        y, _, _ = self.head(codes, out=True, relu=False)
+        self.head(codes, out=y, relu=False)
+        yield
         if keep:
             capture.append({"name": "head", "kind": "conv", "conv": self.head,
                             "codes_in": codes, "residual": None, "out": y, "codes_out": None,
                             "act": None})
-        y = m._avg_pooling(m._swish(y)).flatten(start_dim=1)
-        return m._fc(m._dropout(y))

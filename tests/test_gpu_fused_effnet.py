@@ -215,3 +215,17 @@ def test_fused_se_gate_bit_identical_to_module_path(net, monkeypatch):
             monkeypatch.delenv("TQ_SE_FUSED")
             checked += 1
     assert checked == 16
+
+
+@pytest.mark.parametrize("nstreams", [2, 4])
+def test_fused_efficientnet_b0_stream_split_bit_identical(net, nstreams):
+    """forward_streams: the blocks of image chunks on concurrent HIP streams, the stem and
+    classifier on the whole batch -- logits bit-identical to forward()."""
+    q, x = net
+    fused = tq_fuse.FusedEfficientNet(q)
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    with torch.no_grad():
+        ref = fused(x)
+        got = fused.forward_streams(x, streams)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))

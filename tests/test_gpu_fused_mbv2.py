@@ -124,3 +124,17 @@ def test_fused_mobilenet_v2_teacher_forced(net):
             exp = np.rint(yq.reshape(y.shape) / np.float32(sf2)).astype(np.int64)
             got = _codes(rec["codes_out"], SAMPLE, co).long()
             assert torch.equal(got, torch.from_numpy(exp)), rec["name"]
+
+
+@pytest.mark.parametrize("nstreams", [2, 4])
+def test_fused_mobilenet_v2_stream_split_bit_identical(net, nstreams):
+    """forward_streams: the blocks of image chunks on concurrent HIP streams, the stem and
+    classifier on the whole batch -- logits bit-identical to forward()."""
+    q, x = net
+    fused = tq_fuse.FusedMobileNetV2(q)
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    with torch.no_grad():
+        ref = fused(x)
+        got = fused.forward_streams(x, streams)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))

@@ -181,9 +181,12 @@ def cnn(arch, args, dev):
         if arch in ("mobilenet_v2", "efficientnet_b0"):  # fused executors (tq_fuse.py)
             ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
                   tq_fuse.FusedEfficientNet)(q)
-            tf = timed(lambda: ex(x), args.steps, args.warmup)
+            tf1 = timed(lambda: ex(x), args.steps, args.warmup)
+            streams = [torch.cuda.Stream() for _ in range(2)]
+            tf = timed(lambda: ex.forward_streams(x, streams), args.steps, args.warmup)
             tg = timed_graph(lambda: ex(x), args.steps, args.warmup)
             fused = {"images_per_s": args.batch / tf, "ms_per_step": tf * 1e3,
+                     "streams": 2, "images_per_s_one_stream": args.batch / tf1,
                      "term_pair_macs_per_s": tmacs * args.batch / tf,
                      # the same forward replayed as one hipGraph: with ~50 launches of
                      # ~100 us the eager loop is partly host-bound
@@ -215,13 +218,18 @@ def cnn_fused(arch, steps, warmup, batch, dev):
         tr_layer.set_tr_tracking(q, False)
         ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
               tq_fuse.FusedEfficientNet)(q)
-        tf = timed(lambda: ex(x), steps, warmup)
-        kern = kernel_breakdown(lambda: ex(x), steps, tf)
+        tf1 = timed(lambda: ex(x), steps, warmup)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        # two image chunks on two streams (tq_fuse forward_streams): the measured rate
+        tf = timed(lambda: ex.forward_streams(x, streams), steps, warmup)
+        # per-kernel rooflines from one-stream launches (concurrent launches share the GPU)
+        kern = kernel_breakdown(lambda: ex(x), steps, tf1)
     tp = kern.get("conv2d_termpair")
     if tp is not None:  # 1x1 convs: HBM-bound (algorithmic bytes per launch, fused _Conv)
         tp.update({"bound": "hbm", "mfma_frac": tp.pop("frac"), "frac": tp.pop("hbm_frac", None)})
     dom = max(kern, key=lambda k: kern[k]["share_of_step"])
     return {"images_per_s": batch / tf, "ms_per_step": tf * 1e3, "batch": batch,
+            "streams": 2, "images_per_s_one_stream": batch / tf1,
             "dominant_kernel": dom, "kernels": kern}
 
 
@@ -251,9 +259,15 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--only", choices=("lstm", "mobilenet_v2", "efficientnet_b0"),
                     help="run one config")
+    ap.add_argument("--fused-only", choices=("mobilenet_v2", "efficientnet_b0"),
+                    help="the fused executor of one config alone (profiling runs)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = True
+    if args.fused_only:
+        print(json.dumps(cnn_fused(args.fused_only, args.steps, args.warmup, args.batch, dev)),
+              flush=True)
+        return
     runs = [("lstm", lambda: lstm(args, dev)),
             ("mobilenet_v2", lambda: cnn("mobilenet_v2", args, dev)),
             ("efficientnet_b0", lambda: cnn("efficientnet_b0", args, dev))]
