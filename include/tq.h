@@ -413,6 +413,28 @@ int tq_lstm_seq_f32(const float *gx, const float *w_hh, const float *b_hh, const
                     int64_t hidden, void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
+ * Two stacked LSTM layers' recurrences (TRLSTMLayer's LSTM-650: layer 0 from the term-pair
+ * input projection, layer 1 untouched by the reference's TR) in wavefront order: launch s
+ * runs layer 0's step s and layer 1's step s - 1 in one grid, steps + 1 dependent launches
+ * in all.  Layer 0 as tq_lstm_seq_f32 (gx0 [steps][batch][4 hidden] incl. b_ih0, w_hh0,
+ * b_hh0, h00, c00 -> out0, c_out0); layer 1 computes its own input projection per step:
+ *   gates_t = (out0[t] W_ih1^T + b_ih1) + (h_{t-1} W_hh1^T + b_hh1)
+ * from (h01, c01) -> out1 [steps][batch][hidden], c_out1.  Biases may be NULL.  fp32
+ * arithmetic, 16 fixed-order segments per dot product (the single-layer call's order for
+ * layer 0; layer 1's sums are not those of a separate GEMM + tq_lstm_seq_f32, so its values
+ * match that path to fp32 rounding, not bit for bit).  Returns TQ_ERR_UNSUPPORTED outside
+ * tq_lstm_seq2_supported(batch, hidden) (hidden <= 1024, both layers' staged rows in LDS:
+ * batch <= 39 at hidden 650).  Outputs may not alias the inputs.
+ */
+int tq_lstm_seq2_supported(int64_t batch, int64_t hidden);
+int tq_lstm_seq2_f32(const float *gx0, const float *w_hh0, const float *b_hh0,
+                     const float *h00, const float *c00, const float *w_ih1,
+                     const float *b_ih1, const float *w_hh1, const float *b_hh1,
+                     const float *h01, const float *c01, float *out0, float *out1,
+                     float *c_out0, float *c_out1, int64_t steps, int64_t batch,
+                     int64_t hidden, void *stream);
+
+/*
  * Tracking histogram of the activation calibration, replacing
  *   self.hist_bins += torch.histc(x, self.num_bins, self.minv, self.maxv)
  * of LinearQuantize.forward (tr_layer.py:91-94):

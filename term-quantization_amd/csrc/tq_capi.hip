@@ -755,6 +755,42 @@ int tq_lstm_seq_f32(const float* gx, const float* w_hh, const float* b_hh, const
                     "lstm_seq launch");
 }
 
+int tq_lstm_seq2_supported(int64_t batch, int64_t hidden) {
+  return tq::lstm_seq2_supported(batch, hidden) ? 1 : 0;
+}
+
+int tq_lstm_seq2_f32(const float* gx0, const float* w_hh0, const float* b_hh0,
+                     const float* h00, const float* c00, const float* w_ih1,
+                     const float* b_ih1, const float* w_hh1, const float* b_hh1,
+                     const float* h01, const float* c01, float* out0, float* out1,
+                     float* c_out0, float* c_out1, int64_t steps, int64_t batch,
+                     int64_t hidden, void* stream) {
+  if (steps < 0 || batch < 0 || hidden < 0)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: negative size");
+  if (steps * batch * hidden == 0) return TQ_OK;
+  if (!tq::lstm_seq2_supported(batch, hidden))
+    return fail(TQ_ERR_UNSUPPORTED, "lstm_seq2: hidden <= 1024 and both layers' staged rows "
+                "in one workgroup's LDS (tq_lstm_seq2_supported)");
+  if (!gx0 || !w_hh0 || !h00 || !c00 || !w_ih1 || !w_hh1 || !h01 || !c01 || !out0 || !out1 ||
+      !c_out0 || !c_out1)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: null pointer");
+  const void* ins[] = {gx0, h00, c00, h01, c01};
+  const void* outs[] = {out0, out1, c_out0, c_out1};
+  for (const void* o : outs) {
+    for (const void* i : ins)
+      if (o == i)
+        return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: outputs may not alias the inputs");
+  }
+  if (out0 == out1 || c_out0 == c_out1 || (const void*)c_out0 == (const void*)out1 ||
+      (const void*)c_out1 == (const void*)out0 || (const void*)c_out0 == (const void*)out0 ||
+      (const void*)c_out1 == (const void*)out1)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: outputs may not alias each other");
+  return hip_status(tq::launch_lstm_seq2(gx0, w_hh0, b_hh0, h00, c00, w_ih1, b_ih1, w_hh1,
+                                         b_hh1, h01, c01, out0, out1, c_out0, c_out1, steps,
+                                         batch, hidden, (hipStream_t)stream),
+                    "lstm_seq2 launch");
+}
+
 int tq_histc_f32(const float* x, int64_t numel, int64_t nbins, float minv, float maxv,
                  uint64_t* counts, float* hist, void* stream) {
   if (numel < 0 || nbins < 1 || nbins > (1 << 24))

@@ -108,6 +108,13 @@ hipError_t launch_lstm_cell(const float* gx, const float* hh, float* c, float* h
                             int64_t H, hipStream_t stream);
 // A whole LSTM layer's recurrence: T fused step launches from one call (tq_lstm.hip)
 int64_t lstm_seq_workspace_bytes(int64_t B, int64_t H);
+bool lstm_seq2_supported(int64_t B, int64_t H);
+hipError_t launch_lstm_seq2(const float* gx0, const float* w_hh0, const float* b_hh0,
+                            const float* h00, const float* c00, const float* w_ih1,
+                            const float* b_ih1, const float* w_hh1, const float* b_hh1,
+                            const float* h01, const float* c01, float* out0, float* out1,
+                            float* cT0, float* cT1, int64_t T, int64_t B, int64_t H,
+                            hipStream_t stream);
 hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, const float* h0,
                            const float* c0, float* out, float* cT, int64_t T, int64_t B,
                            int64_t H, void* ws, hipStream_t stream);

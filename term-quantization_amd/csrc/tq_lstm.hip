@@ -237,4 +237,250 @@ hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, cons
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Two stacked layers in wavefront order (tq_lstm_seq2_f32): launch s runs layer 0's step s
+// and layer 1's step s - 1 side by side in one grid (workgroups [0, G) and [G, 2G)), so a
+// 2-layer recurrence of T steps takes T + 1 dependent launches instead of 2T plus the layer-1
+// input-projection GEMM between them.  Layer 1's input projection h0_t W_ih1^T is computed
+// in its step (it depends on layer 0's step t, finished by the previous launch):
+//   layer 1: gates = (x_t W_ih^T + b_ih) + (h_{t-1} W_hh^T + b_hh),  x_t = layer 0's h_t
+// Each dot product is 16 fixed-order segments of L terms, as the one-layer kernel; W rows go
+// straight from L2 into registers (no LDS staging), so a workgroup needs only the staged
+// h_{t-1} (and x_t) rows and the partial sums: <= 80 KB of LDS at LSTM-650, two workgroups
+// per CU, and both layers' grids are resident at once.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+struct LstmRole {
+  const float* gx;      // layer 0: [B][4H] this step's input projection (incl. b_ih)
+  const float* x;       // layer 1: [B][H] this step's input (layer 0's h at the same step)
+  const float* w_ih;    // layer 1: [4H][H]
+  const float* b_ih;    // layer 1: [4H] or nullptr
+  const float* w;       // W_hh [4H][H]
+  const float* b;       // b_hh [4H] or nullptr
+  const float* h_prev;  // [B][H]
+  const float* c_prev;  // [B][H]
+  float* h;             // [B][H]
+  float* c;             // [B][H] (may alias c_prev)
+};
+
+struct LstmStep2Args {
+  LstmRole r[2];
+  int first;  // role of workgroups [0, G): 0, or 1 when layer 0 has no step left
+  int B, H, nu, G;
+};
+
+// LDS floats of a workgroup: h_{t-1} and x rows [B][HP] each, partial sums [2][4 nu][B][16]
+__host__ __device__ constexpr int64_t lstm2_lds_floats(int64_t B, int64_t HP, int64_t nu) {
+  return 2 * B * HP + 2 * 4 * nu * B * kStepSeg;
+}
+
+template <int L, bool X2>
+__device__ __forceinline__ void lstm2_role(const LstmRole& a, int wg, int B, int H, int nu_max,
+                                           float* lds) {
+  constexpr int HP = kStepSeg * L;
+  const int tid = threadIdx.x;
+  const int u0 = wg * nu_max;
+  const int nu = min(nu_max, H - u0);
+  float* hprev = lds;                                   // [B][HP]
+  float* xin = hprev + (int64_t)B * HP;                 // [B][HP] (X2)
+  float* part_h = xin + (int64_t)B * HP;                // [4 nu][B][kStepSeg]
+  float* part_x = part_h + (int64_t)4 * nu_max * B * kStepSeg;
+  const bool cell = tid < B * nu;
+  const int ct = cell ? tid : 0;
+  const int cb = ct / nu, cu = ct - (ct / nu) * nu;
+  float gpre[4], bpre[4], xbpre[4];
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    const int col = gi * H + u0 + cu;
+    gpre[gi] = X2 ? 0.0f : a.gx[(int64_t)cb * 4 * H + col];
+    bpre[gi] = a.b ? a.b[col] : 0.0f;
+    xbpre[gi] = X2 && a.b_ih ? a.b_ih[col] : 0.0f;
+  }
+  const float cprev = a.c_prev[(int64_t)cb * H + u0 + cu];
+  // dot-product role: gate row r (gate r / nu, unit u0 + r % nu), segment s; its W segments
+  // straight into registers (L2-resident rows)
+  const int r = tid / kStepSeg, s = tid % kStepSeg;
+  const bool dot = r < 4 * nu;
+  const int64_t wrow = dot ? (int64_t)((r / nu) * H + u0 + r % nu) * H : 0;
+  float wh[L], wx[X2 ? L : 1];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int j = s * L + i;
+    wh[i] = dot && j < H ? a.w[wrow + j] : 0.0f;
+    if (X2) wx[i] = dot && j < H ? a.w_ih[wrow + j] : 0.0f;
+  }
+  // stage h_{t-1} (and x_t) zero-padded to HP columns, kStageRows rows per batch of loads
+  constexpr int JC = (HP + kStepThreads - 1) / kStepThreads;
+  const int nrow = X2 ? 2 * B : B;
+  for (int q0 = 0; q0 < nrow; q0 += kStageRows) {
+    float v[kStageRows][JC];
+#pragma unroll
+    for (int i = 0; i < kStageRows; ++i) {
+      const int q = min(q0 + i, nrow - 1);  // clamped: in-bounds loads, no branches
+      const float* src = q < B ? a.h_prev + (int64_t)q * H : a.x + (int64_t)(q - B) * H;
+#pragma unroll
+      for (int jj = 0; jj < JC; ++jj) {
+        const int j = tid + jj * kStepThreads;
+        const float x = src[min(j, H - 1)];
+        v[i][jj] = j < H ? x : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kStageRows; ++i) {
+      const int q = q0 + i;
+      if (q >= nrow) break;
+      float* dst = q < B ? hprev + q * HP : xin + (q - B) * HP;
+#pragma unroll
+      for (int jj = 0; jj < JC; ++jj) {
+        const int j = tid + jj * kStepThreads;
+        if (j < HP) dst[j] = v[i][jj];
+      }
+    }
+  }
+  __syncthreads();
+  if (dot) {
+    for (int bb = 0; bb < B; ++bb) {
+      const float* hp = hprev + bb * HP + s * L;
+      float acc0 = 0.0f, acc1 = 0.0f;  // two chains; fixed order (as lstm_step_kernel)
+#pragma unroll
+      for (int i = 0; i + 1 < L; i += 2) {
+        acc0 = fmaf(hp[i], wh[i], acc0);
+        acc1 = fmaf(hp[i + 1], wh[i + 1], acc1);
+      }
+      if (L & 1) acc0 = fmaf(hp[L - 1], wh[L - 1], acc0);
+      part_h[((int64_t)r * B + bb) * kStepSeg + s] = acc0 + acc1;
+      if (X2) {
+        const float* xp = xin + bb * HP + s * L;
+        float x0 = 0.0f, x1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i + 1 < L; i += 2) {
+          x0 = fmaf(xp[i], wx[i], x0);
+          x1 = fmaf(xp[i + 1], wx[i + 1], x1);
+        }
+        if (L & 1) x0 = fmaf(xp[L - 1], wx[L - 1], x0);
+        part_x[((int64_t)r * B + bb) * kStepSeg + s] = x0 + x1;
+      }
+    }
+  }
+  __syncthreads();
+  if (cell) {
+    float gate[4];
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) {
+      const int64_t pi = ((int64_t)(gi * nu + cu) * B + cb) * kStepSeg;
+      float sum = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kStepSeg; ++k) sum += part_h[pi + k];
+      float gxv = gpre[gi];
+      if (X2) {
+        float xs = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kStepSeg; ++k) xs += part_x[pi + k];
+        gxv = xs + xbpre[gi];
+      }
+      gate[gi] = gxv + (sum + bpre[gi]);
+    }
+    const int64_t o = (int64_t)cb * H + u0 + cu;
+    const float c = sigmoid_f(gate[1]) * cprev + sigmoid_f(gate[0]) * tanhf(gate[2]);
+    a.c[o] = c;
+    a.h[o] = sigmoid_f(gate[3]) * tanhf(c);
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(kStepThreads) void lstm_step2_kernel(LstmStep2Args a) {
+  extern __shared__ float step2_lds[];
+  const int role = a.first + (int)(blockIdx.x / a.G);
+  const int wg = (int)(blockIdx.x % a.G);
+  if (role == 0)
+    lstm2_role<L, false>(a.r[0], wg, a.B, a.H, a.nu, step2_lds);
+  else
+    lstm2_role<L, true>(a.r[1], wg, a.B, a.H, a.nu, step2_lds);
+}
+
+template <int L>
+hipError_t launch_lstm_steps2(LstmStep2Args a, const float* gx0, const float* h00,
+                              const float* c00, const float* h01, const float* c01, float* out0,
+                              float* out1, float* cT0, float* cT1, int64_t T,
+                              hipStream_t stream) {
+  constexpr int HP = kStepSeg * L;
+  const int64_t B = a.B, H = a.H;
+  const size_t lds = (size_t)lstm2_lds_floats(B, HP, a.nu) * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_step2_kernel<L>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  for (int64_t s = 0; s <= T; ++s) {
+    const bool have0 = s < T, have1 = s >= 1;
+    if (have0) {  // layer 0, step s
+      LstmRole& r = a.r[0];
+      r.gx = gx0 + s * B * 4 * H;
+      r.h_prev = s == 0 ? h00 : out0 + (s - 1) * B * H;
+      r.c_prev = s == 0 ? c00 : cT0;
+      r.h = out0 + s * B * H;
+      r.c = cT0;
+    }
+    if (have1) {  // layer 1, step s - 1 (its input: layer 0's step s - 1)
+      const int64_t t = s - 1;
+      LstmRole& r = a.r[1];
+      r.x = out0 + t * B * H;
+      r.h_prev = t == 0 ? h01 : out1 + (t - 1) * B * H;
+      r.c_prev = t == 0 ? c01 : cT1;
+      r.h = out1 + t * B * H;
+      r.c = cT1;
+    }
+    a.first = have0 ? 0 : 1;
+    const int grid = a.G * ((have0 ? 1 : 0) + (have1 ? 1 : 0));
+    lstm_step2_kernel<L><<<dim3(grid), kStepThreads, lds, stream>>>(a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool lstm_seq2_supported(int64_t B, int64_t H) {
+  const int64_t L = lstm_seg_len(H);
+  if (B < 1 || H < 1 || L == 0) return false;
+  const int64_t nu = (H + 255) / 256;
+  if (B * nu > kStepThreads) return false;
+  return lstm2_lds_floats(B, kStepSeg * L, nu) * 4 <= 160 * 1024;
+}
+
+hipError_t launch_lstm_seq2(const float* gx0, const float* w_hh0, const float* b_hh0,
+                            const float* h00, const float* c00, const float* w_ih1,
+                            const float* b_ih1, const float* w_hh1, const float* b_hh1,
+                            const float* h01, const float* c01, float* out0, float* out1,
+                            float* cT0, float* cT1, int64_t T, int64_t B, int64_t H,
+                            hipStream_t stream) {
+  if (T == 0 || B == 0 || H == 0) return hipSuccess;
+  LstmStep2Args a = {};
+  a.r[0].w = w_hh0;
+  a.r[0].b = b_hh0;
+  a.r[1].w_ih = w_ih1;
+  a.r[1].b_ih = b_ih1;
+  a.r[1].w = w_hh1;
+  a.r[1].b = b_hh1;
+  a.B = (int)B;
+  a.H = (int)H;
+  a.nu = (int)((H + 255) / 256);
+  a.G = (int)((H + a.nu - 1) / a.nu);
+  switch (lstm_seg_len(H)) {
+#define TQ_SEQ2(LL)                                                                         \
+  case LL:                                                                                   \
+    return launch_lstm_steps2<LL>(a, gx0, h00, c00, h01, c01, out0, out1, cT0, cT1, T, stream);
+    TQ_SEQ2(16)
+    TQ_SEQ2(32)
+    TQ_SEQ2(41)
+    TQ_SEQ2(48)
+    TQ_SEQ2(64)
+#undef TQ_SEQ2
+    default: return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace tq

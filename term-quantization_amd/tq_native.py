@@ -38,6 +38,8 @@ _SIGNATURES = {
     "tq_sync_faults": [ctypes.POINTER(ctypes.c_uint32)],
     "tq_lstm_seq_workspace_bytes": [_i64, _i64],
     "tq_lstm_seq_f32": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp],
+    "tq_lstm_seq2_supported": [_i64, _i64],
+    "tq_lstm_seq2_f32": [_vp] * 15 + [_i64, _i64, _i64, _vp],
     "tq_tr_f32": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_f64": [_vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32, _vp],
     "tq_tr_encode_f32": [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _f32, _i32, _i32, _i32,
@@ -262,6 +264,27 @@ def lstm_seq(gx, w_hh, b_hh, h0, c0, out, c_out):
                                    _stream(gx))
     _check(rc)
     return out
+
+
+def lstm_seq2_supported(batch, hidden):
+    """tq_lstm_seq2_supported: the two-layer wavefront call covers (batch, hidden)."""
+    return bool(lib().tq_lstm_seq2_supported(batch, hidden))
+
+
+def lstm_seq2(gx0, w_hh0, b_hh0, h00, c00, w_ih1, b_ih1, w_hh1, b_hh1, h01, c01, out0, out1,
+              c_out0, c_out1):
+    """Two stacked LSTM layers' recurrences in wavefront order (tq_lstm_seq2_f32: steps + 1
+    launches, layer 1's input projection inside its steps): gx0 [T, B, 4H] (layer 0's input
+    projection incl. b_ih0), weights [4H, H], biases [4H] or None, initial states [B, H],
+    out0 / out1 [T, B, H], c_out0 / c_out1 [B, H]; contiguous fp32 CUDA tensors."""
+    t, b, h4 = gx0.shape
+    with torch.cuda.device(gx0.device):
+        rc = lib().tq_lstm_seq2_f32(
+            _ptr(gx0), _ptr(w_hh0), _ptr(b_hh0), _ptr(h00), _ptr(c00), _ptr(w_ih1),
+            _ptr(b_ih1), _ptr(w_hh1), _ptr(b_hh1), _ptr(h01), _ptr(c01), _ptr(out0),
+            _ptr(out1), _ptr(c_out0), _ptr(c_out1), t, b, h4 // 4, _stream(gx0))
+    _check(rc)
+    return out0, out1
 
 
 def _check(rc):

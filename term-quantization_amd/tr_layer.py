@@ -474,6 +474,20 @@ class TRLSTMLayer(nn.Module):
         # each layer's recurrence in one call (tq_lstm_seq_f32: a fused step kernel per
         # step); layer 0 from TR(h0), TR(c0) with the TR'd W_hh (fp32 on the TR'd values)
         c_last = torch.empty((l.num_layers, B, H), dtype=emb.dtype, device=emb.device)
+        if (l.num_layers == 2 and self._upper is not None and
+                os.environ.get("TQ_LSTM_WAVE", "1") != "0" and
+                os.environ.get("TQ_LSTM_UPPER", "seq") != "miopen" and
+                tq_native.lstm_seq2_supported(B, H)):
+            # both layers in wavefront order (tq_lstm_seq2_f32): layer 1's step t beside
+            # layer 0's step t + 1 in one launch, its input projection inside the step
+            out1 = torch.empty((T, B, H), dtype=emb.dtype, device=emb.device)
+            tq_native.lstm_seq2(gx, l.weight_hh_l0.contiguous(), l.bias_hh_l0.contiguous(),
+                                hq[0].contiguous(), cq[0].contiguous(),
+                                l.weight_ih_l1.contiguous(), l.bias_ih_l1.contiguous(),
+                                l.weight_hh_l1.contiguous(), l.bias_hh_l1.contiguous(),
+                                hq[1].contiguous(), cq[1].contiguous(), out0, out1, c_last[0],
+                                c_last[1])
+            return out1, (torch.stack([out0[T - 1], out1[T - 1]]), c_last)
         tq_native.lstm_seq(gx, l.weight_hh_l0.contiguous(), l.bias_hh_l0.contiguous(),
                            hq[0].contiguous(), cq[0].contiguous(), out0, c_last[0])
         outs = [out0]

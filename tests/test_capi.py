@@ -241,3 +241,30 @@ def test_lstm_seq_argument_validation():
     q = p + 4096
     rc = lib.tq_lstm_seq_f32(p, p, None, p, q, p + 8192, q, 35, 10, 650, None, 0, None)
     assert rc == 1 and b"alias" in lib.tq_last_error()
+
+
+def test_lstm_seq2_argument_validation():
+    """tq_lstm_seq2_f32 rejects shapes outside its domain, null pointers and aliased outputs
+    before any launch."""
+    lib = tq_native.lib()
+    buf = torch.zeros(1 << 16, dtype=torch.float32)
+    p = buf.data_ptr()
+    ptrs = [p + 256 * i for i in range(15)]
+    assert tq_native.lstm_seq2_supported(10, 650)
+    assert not tq_native.lstm_seq2_supported(10, 1100)
+    assert not tq_native.lstm_seq2_supported(100, 650)
+    rc = lib.tq_lstm_seq2_f32(*ptrs, 35, 10, 1100, None)
+    assert rc == 2 and b"hidden <= 1024" in lib.tq_last_error()
+    bad = list(ptrs)
+    bad[3] = None  # h00
+    rc = lib.tq_lstm_seq2_f32(*bad, 35, 10, 650, None)
+    assert rc == 1 and b"null" in lib.tq_last_error()
+    bad = list(ptrs)
+    bad[11] = bad[3]  # out0 aliases h00
+    rc = lib.tq_lstm_seq2_f32(*bad, 35, 10, 650, None)
+    assert rc == 1 and b"alias" in lib.tq_last_error()
+    bad = list(ptrs)
+    bad[14] = bad[13]  # c_out1 aliases c_out0
+    rc = lib.tq_lstm_seq2_f32(*bad, 35, 10, 650, None)
+    assert rc == 1 and b"alias" in lib.tq_last_error()
+    assert lib.tq_lstm_seq2_f32(*ptrs, 0, 10, 650, None) == 0  # empty: no launch

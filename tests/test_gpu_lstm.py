@@ -27,16 +27,19 @@ def _oracle_w(w, bits, g, k):
     return torch.from_numpy(oracle.tr(w.detach().cpu().contiguous().numpy(), sf, bits, g, k))
 
 
-@pytest.mark.parametrize("termpair,seq", [(False, None), (True, "1"), (True, "0"),
-                                          (True, "miopen")])
+@pytest.mark.parametrize("termpair,seq", [(False, None), (True, "1"), (True, "layer"),
+                                          (True, "0"), (True, "miopen")])
 def test_lstm650_tq_chunk_against_oracle(termpair, seq, monkeypatch):
-    """seq (term-pair path): "1" = each layer's recurrence in one persistent launch
-    (tq_lstm_seq_f32, both layers), "0" = per-step launches (a GEMM + tq_lstm_cell_f32 per
-    step, MIOpen for layer 1), "miopen" = the persistent launch for layer 0, MIOpen above."""
+    """seq (term-pair path): "1" (default) = both layers in wavefront order, T + 1 launches
+    (tq_lstm_seq2_f32), "layer" = each layer's recurrence from one call (tq_lstm_seq_f32,
+    TQ_LSTM_WAVE=0), "0" = per-step launches (a GEMM + tq_lstm_cell_f32 per step, MIOpen for
+    layer 1), "miopen" = the one-call recurrence for layer 0, MIOpen above."""
     import evaluate_lstm
     import tq_native
     if seq == "miopen":
         monkeypatch.setenv("TQ_LSTM_UPPER", "miopen")
+    elif seq == "layer":
+        monkeypatch.setenv("TQ_LSTM_WAVE", "0")
     elif seq is not None:
         monkeypatch.setenv("TQ_LSTM_SEQ", seq)
     tq_native.sync_faults()
