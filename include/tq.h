@@ -420,11 +420,12 @@ int tq_lstm_seq_f32(const float *gx, const float *w_hh, const float *b_hh, const
  * b_hh0, h00, c00 -> out0, c_out0); layer 1 computes its own input projection per step:
  *   gates_t = (out0[t] W_ih1^T + b_ih1) + (h_{t-1} W_hh1^T + b_hh1)
  * from (h01, c01) -> out1 [steps][batch][hidden], c_out1.  Biases may be NULL.  fp32
- * arithmetic, 16 fixed-order segments per dot product (the single-layer call's order for
- * layer 0; layer 1's sums are not those of a separate GEMM + tq_lstm_seq_f32, so its values
- * match that path to fp32 rounding, not bit for bit).  Returns TQ_ERR_UNSUPPORTED outside
- * tq_lstm_seq2_supported(batch, hidden) (hidden <= 1024, both layers' staged rows in LDS:
- * batch <= 39 at hidden 650).  Outputs may not alias the inputs.
+ * arithmetic, 16 fixed-order partial sums per dot product over interleaved column pairs (so
+ * layer 0's order differs from tq_lstm_seq_f32's, and layer 1's sums are not those of a
+ * separate GEMM + tq_lstm_seq_f32: both match that path to fp32 rounding, not bit for bit).
+ * Returns TQ_ERR_UNSUPPORTED outside tq_lstm_seq2_supported(batch, hidden) (even hidden <=
+ * 1024, both layers' staged rows in one workgroup's LDS: batch <= 23 at hidden 650); weights
+ * 8-byte aligned.  Outputs may not alias the inputs.
  */
 int tq_lstm_seq2_supported(int64_t batch, int64_t hidden);
 int tq_lstm_seq2_f32(const float *gx0, const float *w_hh0, const float *b_hh0,

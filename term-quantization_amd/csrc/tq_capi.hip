@@ -769,11 +769,13 @@ int tq_lstm_seq2_f32(const float* gx0, const float* w_hh0, const float* b_hh0,
     return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: negative size");
   if (steps * batch * hidden == 0) return TQ_OK;
   if (!tq::lstm_seq2_supported(batch, hidden))
-    return fail(TQ_ERR_UNSUPPORTED, "lstm_seq2: hidden <= 1024 and both layers' staged rows "
-                "in one workgroup's LDS (tq_lstm_seq2_supported)");
+    return fail(TQ_ERR_UNSUPPORTED, "lstm_seq2: even hidden <= 1024 and both layers' staged "
+                "rows in one workgroup's LDS (tq_lstm_seq2_supported)");
   if (!gx0 || !w_hh0 || !h00 || !c00 || !w_ih1 || !w_hh1 || !h01 || !c01 || !out0 || !out1 ||
       !c_out0 || !c_out1)
     return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: null pointer");
+  if (((uintptr_t)w_hh0 | (uintptr_t)w_ih1 | (uintptr_t)w_hh1) & 7)
+    return fail(TQ_ERR_INVALID_ARGUMENT, "lstm_seq2: weights must be 8-byte aligned");
   const void* ins[] = {gx0, h00, c00, h01, c01};
   const void* outs[] = {out0, out1, c_out0, c_out1};
   for (const void* o : outs) {

@@ -245,10 +245,12 @@ hipError_t launch_lstm_seq(const float* gx, const float* w, const float* b, cons
 // input-projection GEMM between them.  Layer 1's input projection h0_t W_ih1^T is computed
 // in its step (it depends on layer 0's step t, finished by the previous launch):
 //   layer 1: gates = (x_t W_ih^T + b_ih) + (h_{t-1} W_hh^T + b_hh),  x_t = layer 0's h_t
-// Each dot product is 16 fixed-order segments of L terms, as the one-layer kernel; W rows go
-// straight from L2 into registers (no LDS staging), so a workgroup needs only the staged
-// h_{t-1} (and x_t) rows and the partial sums: <= 80 KB of LDS at LSTM-650, two workgroups
-// per CU, and both layers' grids are resident at once.
+// Each dot product is 16 fixed-order partial sums; thread s of a gate row takes the column
+// pairs (2 (s + 16 i), 2 (s + 16 i) + 1), i < P, so the wave's 8-byte W loads cover whole
+// 64-byte runs of each row: W rows go straight from L2 into registers (no LDS staging, rows
+// are 8-byte aligned for even H), and a workgroup needs only the staged h_{t-1} (and x_t) rows
+// and the partial sums: <= 80 KB of LDS at LSTM-650, two workgroups per CU, both layers'
+// grids resident at once.
 // ---------------------------------------------------------------------------------------
 namespace {
 
@@ -276,10 +278,10 @@ __host__ __device__ constexpr int64_t lstm2_lds_floats(int64_t B, int64_t HP, in
   return 2 * B * HP + 2 * 4 * nu * B * kStepSeg;
 }
 
-template <int L, bool X2>
+template <int P, bool X2>
 __device__ __forceinline__ void lstm2_role(const LstmRole& a, int wg, int B, int H, int nu_max,
                                            float* lds) {
-  constexpr int HP = kStepSeg * L;
+  constexpr int HP = 2 * kStepSeg * P;  // staged row length (zero-padded)
   const int tid = threadIdx.x;
   const int u0 = wg * nu_max;
   const int nu = min(nu_max, H - u0);
@@ -304,12 +306,14 @@ __device__ __forceinline__ void lstm2_role(const LstmRole& a, int wg, int B, int
   const int r = tid / kStepSeg, s = tid % kStepSeg;
   const bool dot = r < 4 * nu;
   const int64_t wrow = dot ? (int64_t)((r / nu) * H + u0 + r % nu) * H : 0;
-  float wh[L], wx[X2 ? L : 1];
+  float2 wh[P], wx[X2 ? P : 1];
 #pragma unroll
-  for (int i = 0; i < L; ++i) {
-    const int j = s * L + i;
-    wh[i] = dot && j < H ? a.w[wrow + j] : 0.0f;
-    if (X2) wx[i] = dot && j < H ? a.w_ih[wrow + j] : 0.0f;
+  for (int i = 0; i < P; ++i) {
+    const int j = 2 * (s + kStepSeg * i);  // H even: a pair is in the row or wholly past it
+    const bool ok = dot && j < H;
+    wh[i] = ok ? *reinterpret_cast<const float2*>(a.w + wrow + j) : make_float2(0.f, 0.f);
+    if (X2)
+      wx[i] = ok ? *reinterpret_cast<const float2*>(a.w_ih + wrow + j) : make_float2(0.f, 0.f);
   }
   // stage h_{t-1} (and x_t) zero-padded to HP columns, kStageRows rows per batch of loads
   constexpr int JC = (HP + kStepThreads - 1) / kStepThreads;
@@ -342,24 +346,24 @@ __device__ __forceinline__ void lstm2_role(const LstmRole& a, int wg, int B, int
   __syncthreads();
   if (dot) {
     for (int bb = 0; bb < B; ++bb) {
-      const float* hp = hprev + bb * HP + s * L;
-      float acc0 = 0.0f, acc1 = 0.0f;  // two chains; fixed order (as lstm_step_kernel)
+      const float2* hp = reinterpret_cast<const float2*>(hprev + bb * HP) + s;
+      float acc0 = 0.0f, acc1 = 0.0f;  // two chains (even / odd columns); fixed order
 #pragma unroll
-      for (int i = 0; i + 1 < L; i += 2) {
-        acc0 = fmaf(hp[i], wh[i], acc0);
-        acc1 = fmaf(hp[i + 1], wh[i + 1], acc1);
+      for (int i = 0; i < P; ++i) {
+        const float2 hv = hp[kStepSeg * i];
+        acc0 = fmaf(hv.x, wh[i].x, acc0);
+        acc1 = fmaf(hv.y, wh[i].y, acc1);
       }
-      if (L & 1) acc0 = fmaf(hp[L - 1], wh[L - 1], acc0);
       part_h[((int64_t)r * B + bb) * kStepSeg + s] = acc0 + acc1;
       if (X2) {
-        const float* xp = xin + bb * HP + s * L;
+        const float2* xp = reinterpret_cast<const float2*>(xin + bb * HP) + s;
         float x0 = 0.0f, x1 = 0.0f;
 #pragma unroll
-        for (int i = 0; i + 1 < L; i += 2) {
-          x0 = fmaf(xp[i], wx[i], x0);
-          x1 = fmaf(xp[i + 1], wx[i + 1], x1);
+        for (int i = 0; i < P; ++i) {
+          const float2 xv = xp[kStepSeg * i];
+          x0 = fmaf(xv.x, wx[i].x, x0);
+          x1 = fmaf(xv.y, wx[i].y, x1);
         }
-        if (L & 1) x0 = fmaf(xp[L - 1], wx[L - 1], x0);
         part_x[((int64_t)r * B + bb) * kStepSeg + s] = x0 + x1;
       }
     }
@@ -389,28 +393,35 @@ __device__ __forceinline__ void lstm2_role(const LstmRole& a, int wg, int B, int
   }
 }
 
-template <int L>
+template <int P>
 __global__ __launch_bounds__(kStepThreads) void lstm_step2_kernel(LstmStep2Args a) {
   extern __shared__ float step2_lds[];
   const int role = a.first + (int)(blockIdx.x / a.G);
   const int wg = (int)(blockIdx.x % a.G);
   if (role == 0)
-    lstm2_role<L, false>(a.r[0], wg, a.B, a.H, a.nu, step2_lds);
+    lstm2_role<P, false>(a.r[0], wg, a.B, a.H, a.nu, step2_lds);
   else
-    lstm2_role<L, true>(a.r[1], wg, a.B, a.H, a.nu, step2_lds);
+    lstm2_role<P, true>(a.r[1], wg, a.B, a.H, a.nu, step2_lds);
 }
 
-template <int L>
+// column pairs per thread of the two-layer kernel: 32 P >= H (0: H outside its domain)
+static int lstm2_pairs(int64_t H) {
+  if (H < 2 || (H & 1)) return 0;
+  const int64_t p = (H + 31) / 32;
+  return p <= 8 ? 8 : p <= 16 ? 16 : p <= 21 ? 21 : p <= 24 ? 24 : p <= 32 ? 32 : 0;
+}
+
+template <int P>
 hipError_t launch_lstm_steps2(LstmStep2Args a, const float* gx0, const float* h00,
                               const float* c00, const float* h01, const float* c01, float* out0,
                               float* out1, float* cT0, float* cT1, int64_t T,
                               hipStream_t stream) {
-  constexpr int HP = kStepSeg * L;
+  constexpr int HP = 2 * kStepSeg * P;
   const int64_t B = a.B, H = a.H;
   const size_t lds = (size_t)lstm2_lds_floats(B, HP, a.nu) * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_step2_kernel<L>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_step2_kernel<P>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -436,7 +447,7 @@ hipError_t launch_lstm_steps2(LstmStep2Args a, const float* gx0, const float* h0
     }
     a.first = have0 ? 0 : 1;
     const int grid = a.G * ((have0 ? 1 : 0) + (have1 ? 1 : 0));
-    lstm_step2_kernel<L><<<dim3(grid), kStepThreads, lds, stream>>>(a);
+    lstm_step2_kernel<P><<<dim3(grid), kStepThreads, lds, stream>>>(a);
   }
   return hipGetLastError();
 }
@@ -444,11 +455,11 @@ hipError_t launch_lstm_steps2(LstmStep2Args a, const float* gx0, const float* h0
 }  // namespace
 
 bool lstm_seq2_supported(int64_t B, int64_t H) {
-  const int64_t L = lstm_seg_len(H);
-  if (B < 1 || H < 1 || L == 0) return false;
+  const int64_t P = lstm2_pairs(H);
+  if (B < 1 || P == 0) return false;
   const int64_t nu = (H + 255) / 256;
   if (B * nu > kStepThreads) return false;
-  return lstm2_lds_floats(B, kStepSeg * L, nu) * 4 <= 160 * 1024;
+  return lstm2_lds_floats(B, 2 * kStepSeg * P, nu) * 4 <= 160 * 1024;
 }
 
 hipError_t launch_lstm_seq2(const float* gx0, const float* w_hh0, const float* b_hh0,
@@ -469,15 +480,15 @@ hipError_t launch_lstm_seq2(const float* gx0, const float* w_hh0, const float* b
   a.H = (int)H;
   a.nu = (int)((H + 255) / 256);
   a.G = (int)((H + a.nu - 1) / a.nu);
-  switch (lstm_seg_len(H)) {
-#define TQ_SEQ2(LL)                                                                         \
-  case LL:                                                                                   \
-    return launch_lstm_steps2<LL>(a, gx0, h00, c00, h01, c01, out0, out1, cT0, cT1, T, stream);
+  switch (lstm2_pairs(H)) {
+#define TQ_SEQ2(PP)                                                                         \
+  case PP:                                                                                   \
+    return launch_lstm_steps2<PP>(a, gx0, h00, c00, h01, c01, out0, out1, cT0, cT1, T, stream);
+    TQ_SEQ2(8)
     TQ_SEQ2(16)
+    TQ_SEQ2(21)  // H = 650
+    TQ_SEQ2(24)
     TQ_SEQ2(32)
-    TQ_SEQ2(41)
-    TQ_SEQ2(48)
-    TQ_SEQ2(64)
 #undef TQ_SEQ2
     default: return hipErrorInvalidValue;
   }
