@@ -202,7 +202,7 @@ def cnn(arch, args, dev):
             "kernels": kernels, "fused_executor": fused}
 
 
-def cnn_fused(arch, steps, warmup, batch, dev):
+def cnn_fused(arch, steps, warmup, batch, dev, nstreams=2):
     """The fused executor of a depthwise config alone (bench.py's d4 key): images/s and the
     per-kernel rooflines.  Every term-pair conv of these executors is a 1x1 conv with
     Cin <= 960 whose bytes outweigh its products (codes in, fp32/codes out), so it is priced
@@ -219,8 +219,8 @@ def cnn_fused(arch, steps, warmup, batch, dev):
         ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
               tq_fuse.FusedEfficientNet)(q)
         tf1 = timed(lambda: ex(x), steps, warmup)
-        streams = [torch.cuda.Stream() for _ in range(2)]
-        # two image chunks on two streams (tq_fuse forward_streams): the measured rate
+        streams = [torch.cuda.Stream() for _ in range(nstreams)]
+        # image chunks on their own streams (tq_fuse forward_streams): the measured rate
         tf = timed(lambda: ex.forward_streams(x, streams), steps, warmup)
         # per-kernel rooflines from one-stream launches (concurrent launches share the GPU)
         kern = kernel_breakdown(lambda: ex(x), steps, tf1)
@@ -229,7 +229,7 @@ def cnn_fused(arch, steps, warmup, batch, dev):
         tp.update({"bound": "hbm", "mfma_frac": tp.pop("frac"), "frac": tp.pop("hbm_frac", None)})
     dom = max(kern, key=lambda k: kern[k]["share_of_step"])
     return {"images_per_s": batch / tf, "ms_per_step": tf * 1e3, "batch": batch,
-            "streams": 2, "images_per_s_one_stream": batch / tf1,
+            "streams": nstreams, "images_per_s_one_stream": batch / tf1,
             "dominant_kernel": dom, "kernels": kern}
 
 
@@ -261,12 +261,13 @@ def main():
                     help="run one config")
     ap.add_argument("--fused-only", choices=("mobilenet_v2", "efficientnet_b0"),
                     help="the fused executor of one config alone (profiling runs)")
+    ap.add_argument("--streams", type=int, default=2, help="image chunks / streams (fused-only)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = True
     if args.fused_only:
-        print(json.dumps(cnn_fused(args.fused_only, args.steps, args.warmup, args.batch, dev)),
-              flush=True)
+        print(json.dumps(cnn_fused(args.fused_only, args.steps, args.warmup, args.batch, dev,
+                                   args.streams)), flush=True)
         return
     runs = [("lstm", lambda: lstm(args, dev)),
             ("mobilenet_v2", lambda: cnn("mobilenet_v2", args, dev)),
