@@ -302,6 +302,28 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
     else return (uint32_t)(((sbase + tt) % NR) * kRingSlot);
   };
 
+  // residual of pixel block bn of the current tile (FAST epilogue): lane channels cl + 32 bm +
+  // 8 q + [0, 4) of its pixel, zero where the pixel or channel is past the tensor
+  auto load_res = [&](const RingTile& tl, int bn, float4 (&rv)[2][4])
+      __attribute__((always_inline)) {
+    const int cl = tl.m0 + wm + 4 * hh;
+    const int j = wn + 32 * bn + r32;
+    const int64_t p = tl.p0 + j;
+    const bool okp = j < BNv && p < a.P;
+    const int64_t pc = okp ? p * a.Cout + cl : 0;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = RING_AB != 10 && a.residual && okp && cl + 32 * bm + 8 * q < a.Cout;
+        rv[bm][q] = ok ? *reinterpret_cast<const float4*>(a.residual + pc + 32 * bm + 8 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  };
+  // (!FLUSH: pixel block 0's residual is loaded during the tile's last K-step, block 1's
+  // before block 0's epilogue -- their HBM latency hides behind MFMAs / block 0's VALU)
+  float4 rv_pre[2][4];
+
   float16v accf[2][2];
   int acci[FLUSH ? 2 : 1][2][16];
   half8 fa[2][2], fb[2][2];  // [buffer][block]: fragments of one 16-code substep
@@ -360,6 +382,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
         else
           issue_w(nm0, t + NR - 1 - kRingTaps, nc, 0, nlive, slot_off(t + NR - 1));
         if constexpr (t < PI) issue_piece(t, nsrc0, npx, buf ^ 1);
+        if constexpr (FAST && !FLUSH && t == kRingTaps - 1) {
+          if (last_chunk) load_res(cur, 0, rv_pre);
+        }
         // (3) B addresses of step s+1 (next tap, or tap 0 of the next chunk's buffer)
         uint32_t bnx[2];
 #pragma unroll
@@ -438,7 +463,8 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
     if constexpr (FAST) {
       const int cl = cur.m0 + wm + 4 * hh;  // the lane's first channel
       const double* cf = coef + 2 * cl;
-      // one pixel block's residual loads first (2 round trips per tile instead of 4)
+      // one pixel block's residual loads at a time (FLUSH: both blocks' would spill)
+      float4 rv_next[2][4];
       static_for<0, 2>([&](auto bnc) __attribute__((always_inline)) {
         constexpr int bn = decltype(bnc)::value;
         const int j = wn + 32 * bn + r32;
@@ -446,14 +472,20 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
         const bool okp = j < BNv && p < a.P;
         const int64_t pc = okp ? p * a.Cout + cl : 0;
         float4 rv[2][4];
+        if constexpr (FLUSH) {
+          load_res(cur, bn, rv);
+        } else if constexpr (bn == 0) {
+          load_res(cur, 1, rv_next);  // block 1's loads in flight during block 0
 #pragma unroll
-        for (int bm = 0; bm < 2; ++bm)
+          for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const bool ok = RING_AB != 10 && a.residual && okp && cl + 32 * bm + 8 * q < a.Cout;
-            rv[bm][q] = ok ? *reinterpret_cast<const float4*>(a.residual + pc + 32 * bm + 8 * q)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
+            for (int q = 0; q < 4; ++q) rv[bm][q] = rv_pre[bm][q];
+        } else {
+#pragma unroll
+          for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rv[bm][q] = rv_next[bm][q];
+        }
         if (!okp || (RING_AB == 4 && a.out != (float*)p)) return;
 #pragma unroll
         for (int bm = 0; bm < 2; ++bm) {
