@@ -268,3 +268,22 @@ def test_lstm_seq2_argument_validation():
     rc = lib.tq_lstm_seq2_f32(*bad, 35, 10, 650, None)
     assert rc == 1 and b"alias" in lib.tq_last_error()
     assert lib.tq_lstm_seq2_f32(*ptrs, 0, 10, 650, None) == 0  # empty: no launch
+
+
+def test_se_gate_argument_validation():
+    """tq_se_gate_f32 rejects bad shapes, null buffers, wide activations and channel counts
+    past one workgroup's LDS before any launch; n = 0 is a no-op."""
+    lib = tq_native.lib()
+    buf = torch.zeros(1 << 12, dtype=torch.float32)
+    p = buf.data_ptr()
+    args = lambda n, c, cse, br=9, be=9, xp=p: (xp, n, c, p, cse, 1.0, None, 0.1, br, 3, p, 1.0,
+                                                 None, 0.1, be, 3, p, None)
+    rc = lib.tq_se_gate_f32(*args(4, 0, 8))
+    assert rc == 1 and b"bad shape" in lib.tq_last_error()
+    rc = lib.tq_se_gate_f32(*args(4, 96, 8, xp=None))
+    assert rc == 1 and b"null" in lib.tq_last_error()
+    rc = lib.tq_se_gate_f32(*args(4, 96, 8, br=15))
+    assert rc == 2 and b"<= 14" in lib.tq_last_error()
+    rc = lib.tq_se_gate_f32(*args(4, 20000, 8))
+    assert rc == 2 and b"LDS" in lib.tq_last_error()
+    assert lib.tq_se_gate_f32(*args(0, 96, 8)) == 0
