@@ -203,6 +203,8 @@ bool conv_direct_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream);
 // MFMA tap-ring engine (tr_conv_ring.hip): 3x3 stride-1 "same" convs, Cp % 64 == 0, NHWC out,
 // persistent workgroups streaming K-steps across tiles.
+bool conv_xp_eligible(const ConvArgs& a, int out_nhwc);
+hipError_t launch_conv2d_xp(const ConvArgs& a, hipStream_t stream);
 bool conv_ring_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_ring(const ConvArgs& a, hipStream_t stream);
 // MFMA row-strip engine (tr_conv_strip.hip): 3x3 stride-1 pad-1 convs with 64 -> 64 channels,

@@ -481,7 +481,8 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // 11 row strip (tr_conv_strip.hip: 3x3/1, 64 -> 64 channels, W <= 56; else the default).
 // 12 persistent pointwise (tr_conv_direct.hip: 1x1, K <= 3 K-steps; else the default).
 // 13 tap ring (tr_conv_ring.hip: 3x3/1 "same", Cp % 64 == 0, Wo <= 256; else the default).
-int conv_mfma_num_configs() { return 13; }
+// 14 expand (tr_conv_xp.hip: 1x1/1, one or two K-steps, weights <= 64 KB; else the default).
+int conv_mfma_num_configs() { return 14; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
@@ -503,6 +504,14 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   const char* pw = getenv("TQ_PW");  // read per launch: tests switch it
   if ((cfg == 11 || (cfg < 0 && pw && atoi(pw) == 1)) && conv_pw_eligible(a, out_nhwc))
     return launch_conv2d_pw(a, stream);
+  // expand engine: config 14, and the default for the 1x1 convs it takes (MobileNet-V2 /
+  // EfficientNet-b0 expand convs: 112^2 x 16 -> 96 534 -> 408 us, tools/gpu_expand_probe.sh);
+  // TQ_XP=0 / 1 forces it off / on (read per launch: tests switch it)
+  const char* xp = getenv("TQ_XP");
+  const bool xp_on = xp ? atoi(xp) == 1 : true;
+  if ((cfg == 13 || (cfg < 0 && xp_on)) && conv_xp_eligible(a, out_nhwc))
+    return launch_conv2d_xp(a, stream);
+  if (cfg == 13) cfg = -1;
   if (a.relu == kActSwish) {  // the swish epilogue exists on the direct engine only
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
     return launch_conv2d_direct(a, 1, stream);
