@@ -12,11 +12,11 @@
 // Why a separate engine.  The direct engine gives each workgroup one 64 x 128 tile: weight
 // DMA, activation loads, code tables, one K-step, epilogue; a 112^2 x 16 -> 96 tile lives ~8 us
 // of which ~3.3 us is that setup, at ~3 resident workgroups per CU.  Here:
-//   * a persistent workgroup stages ALL the layer's weights (NKS x MT slots of 64 rows,
-//     swizzled as the direct engine's), the epilogue coefficients of every channel and the
-//     code tables once;
+//   * a persistent workgroup stages the weights of its Cout group (NKS x MT slots of 64 rows,
+//     swizzled as the direct engine's, <= 32 KB: all of Cout, or MG groups of MT 64-row tiles
+//     for wider layers), the group's epilogue coefficients and the code tables once;
 //   * then each wave works alone (no barrier in the loop): a work item is 32 output pixels x
-//     every Cout tile; its activation fragments (NKS x 4 x 16 bytes per lane) come straight
+//     every Cout tile of the group; its activation fragments (NKS x 4 x 16 bytes per lane) come straight
 //     from HBM into registers, and the NEXT item's are loaded before this item's MFMAs and
 //     epilogues run;
 //   * the epilogue reads the accumulators in the MFMA layout (lane = 4 consecutive channels
@@ -39,16 +39,32 @@ constexpr int kXpSlot = 64 * 8;                 // u32x4 per weight slot: 64 row
 constexpr int kXpMaxWeightBytes = 32 * 1024;    // staged weights per workgroup (48 KB of
                                                 // them left 2 workgroups per CU: slower than
                                                 // the direct engine on 64 -> 384)
+// Cout groups a launch may be split into (TQ_XP_GROUPS, read per launch; default 1 = layers
+// whose weights fit one workgroup): groups re-read the activations, and measured slower than
+// the direct engine on 64 -> 384, 96 -> 576 and 112 -> 672 at 14^2 (46 / 53 / 68 vs 36 / 50 /
+// 59 us), faster only on 80 -> 480 (44 vs 46 us): profiles/r04_expand_probe.txt
+int xp_max_groups() {
+  const char* g = getenv("TQ_XP_GROUPS");
+  return g && atoi(g) > 0 ? atoi(g) : 1;
+}
 
 // LDS bytes of a launch: weights, coefficients, code tables.
 int64_t xp_lds_bytes(const ConvArgs& a, int nks, int mt) {
   return (int64_t)nks * mt * kXpSlot * 16 + (int64_t)mt * 64 * 16 + conv_lut_bytes(a);
 }
 
+// 64-row Cout tiles per workgroup (the weight budget) and the number of Cout groups.
+void xp_groups(const ConvArgs& a, int nks, int* mt, int* mg) {
+  const int tiles = (a.Cout + 63) / 64;
+  const int per = kXpMaxWeightBytes / (nks * kXpSlot * 16);
+  *mt = tiles < per ? tiles : per;
+  *mg = (tiles + *mt - 1) / *mt;
+}
+
 // 5 waves per SIMD at one K-step (90 VGPRs, no spills; 6 spill), 4 at two
 template <int NKS, bool SWISH>
 __global__ __launch_bounds__(kXpThreads) __attribute__((amdgpu_waves_per_eu(NKS == 1 ? 5 : 4)))
-void conv2d_tp_xp_kernel(ConvArgs a, int MT) {
+void conv2d_tp_xp_kernel(ConvArgs a, int MT, int MG) {
   extern __shared__ __attribute__((aligned(16))) u32x4 xp_lds[];
   u32x4* wl = xp_lds;                                                    // [NKS][MT][swz]
   double* coef = reinterpret_cast<double*>(wl + (int64_t)NKS * MT * kXpSlot);  // [MT 64][2]
@@ -60,6 +76,8 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT) {
   const int r32 = lane & 31;
   const int hh = lane >> 5;
   const int cpad = MT * 64;
+  const int grp = blockIdx.x % MG;  // this workgroup's Cout group: channels [mbase, + cpad)
+  const int mbase = grp * cpad;
   const uint16_t* __restrict__ wg = reinterpret_cast<const uint16_t*>(a.w);
   const uint16_t* __restrict__ xg = reinterpret_cast<const uint16_t*>(a.x);
 
@@ -71,21 +89,24 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT) {
     const int ks = (i >> 3) / cpad;
     const int mt = row >> 6, r = row & 63;
     u32x4 v = (u32x4)0u;
-    if (row < a.Cout)
-      v = *reinterpret_cast<const u32x4*>(wg + (int64_t)row * a.Kp + ks * kKStep + 8 * u);
+    if (mbase + row < a.Cout)
+      v = *reinterpret_cast<const u32x4*>(wg + (int64_t)(mbase + row) * a.Kp + ks * kKStep +
+                                          8 * u);
     wl[(ks * MT + mt) * kXpSlot + swz(r, u)] = v;
   }
   for (int i = tid; i < cpad; i += kXpThreads) {
-    const bool ok = i < a.Cout;
-    coef[2 * i] = ok ? (a.ch_scale ? a.ch_scale[i] : a.scale) : 0.0;
-    coef[2 * i + 1] = ok ? (a.ch_scale ? a.ch_shift[i] : (a.bias ? (double)a.bias[i] : 0.0))
+    const int c = mbase + i;
+    const bool ok = c < a.Cout;
+    coef[2 * i] = ok ? (a.ch_scale ? a.ch_scale[c] : a.scale) : 0.0;
+    coef[2 * i + 1] = ok ? (a.ch_scale ? a.ch_shift[c] : (a.bias ? (double)a.bias[c] : 0.0))
                          : 0.0;
   }
   __syncthreads();  // weights, coefficients, code tables: no barrier after this
 
   const int64_t ntile = (a.P + 31) / 32;
-  const int64_t nwave = (int64_t)gridDim.x * (kXpThreads / 64);
-  const int64_t w0 = (int64_t)blockIdx.x * (kXpThreads / 64) + (tid >> 6);
+  // the group's workgroups (gridDim.x is a multiple of MG) walk every pixel item
+  const int64_t nwave = (int64_t)(gridDim.x / MG) * (kXpThreads / 64);
+  const int64_t w0 = (int64_t)(blockIdx.x / MG) * (kXpThreads / 64) + (tid >> 6);
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page);
 
   // B fragments of pixel tile t for this lane (pixel t 32 + r32, codes 8 hh + 16 k of each
@@ -113,7 +134,7 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT) {
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
       for (int bm = 0; bm < 2; ++bm) {
-        const int m0 = mt * 64 + 32 * bm;
+        const int m0 = mbase + mt * 64 + 32 * bm;
         if (m0 >= a.Cout) break;  // wave-uniform
         float16v acc;
 #pragma unroll
@@ -137,8 +158,8 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             acc4[e] = (int)acc[4 * q + e];
-            sc[e] = (coef_t)coef[2 * (co + e)];
-            sh[e] = (coef_t)coef[2 * (co + e) + 1];
+            sc[e] = (coef_t)coef[2 * (co - mbase + e)];
+            sh[e] = (coef_t)coef[2 * (co - mbase + e) + 1];
           }
           emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, nores, lut_a, lut_b);
         }
@@ -152,7 +173,9 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT) {
 }
 
 template <int NKS, bool SWISH>
-hipError_t launch_xp_cfg(const ConvArgs& a, int mt, hipStream_t stream) {
+hipError_t launch_xp_cfg(const ConvArgs& a, hipStream_t stream) {
+  int mt, mg;
+  xp_groups(a, NKS, &mt, &mg);
   const size_t lds = (size_t)xp_lds_bytes(a, NKS, mt);
   const void* fn = reinterpret_cast<const void*>(&conv2d_tp_xp_kernel<NKS, SWISH>);
   static bool attr_set = false;
@@ -167,37 +190,40 @@ hipError_t launch_xp_cfg(const ConvArgs& a, int mt, hipStream_t stream) {
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kXpThreads, lds);
   if (e != hipSuccess) return e;
   if (per_cu < 1) per_cu = 1;
-  const char* genv = getenv("TQ_XP_GRID");  // tests: few workgroups, many items each
-  int64_t grid = genv && atoi(genv) > 0 ? atoi(genv) : (int64_t)per_cu * device_cus();
+  // workgroups per Cout group (TQ_XP_GRID: tests, few workgroups with many items each)
+  const char* genv = getenv("TQ_XP_GRID");
+  int64_t per_grp = genv && atoi(genv) > 0 ? atoi(genv)
+                                           : ((int64_t)per_cu * device_cus() + mg - 1) / mg;
   const int64_t items = (a.P + 31) / 32;
   const int64_t need = (items + kXpThreads / 64 - 1) / (kXpThreads / 64);
-  if (grid > need) grid = need;
-  conv2d_tp_xp_kernel<NKS, SWISH><<<dim3((unsigned)grid), kXpThreads, lds, stream>>>(a, mt);
+  if (per_grp > need) per_grp = need;
+  if (per_grp < 1) per_grp = 1;
+  conv2d_tp_xp_kernel<NKS, SWISH>
+      <<<dim3((unsigned)(per_grp * mg)), kXpThreads, lds, stream>>>(a, mt, mg);
   return hipGetLastError();
 }
 
 }  // namespace
 
 // 1x1 stride-1 pad-0 NHWC convs with one or two K-steps in one exact window, no residual and
-// no fused downsample, Cout % 4 == 0, and the whole weight matrix within 64 KB of LDS.
+// no fused downsample, Cout % 4 == 0, at most kXpMaxGroups Cout groups.
 bool conv_xp_eligible(const ConvArgs& a, int out_nhwc) {
   const int nks = a.Kp / kKStep;
-  const int mt = (a.Cout + 63) / 64;
-  return out_nhwc && a.KH == 1 && a.KW == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 &&
-         a.pw == 0 && a.Cp % 8 == 0 && a.Kp % kKStep == 0 && (nks == 1 || nks == 2) &&
-         (a.kc_steps == 0 || a.kc_steps >= nks) && a.residual == nullptr &&
-         a.ds_x == nullptr && (a.Cout & 3) == 0 &&
-         (int64_t)nks * mt * kXpSlot * 16 <= kXpMaxWeightBytes;
+  if (!(out_nhwc && a.KH == 1 && a.KW == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 &&
+        a.pw == 0 && a.Cp % 8 == 0 && a.Kp % kKStep == 0 && (nks == 1 || nks == 2) &&
+        (a.kc_steps == 0 || a.kc_steps >= nks) && a.residual == nullptr &&
+        a.ds_x == nullptr && (a.Cout & 3) == 0 && a.Cout > 0))
+    return false;
+  int mt, mg;
+  xp_groups(a, nks, &mt, &mg);
+  return mg <= xp_max_groups();
 }
 
 hipError_t launch_conv2d_xp(const ConvArgs& a, hipStream_t stream) {
   const int nks = a.Kp / kKStep;
-  const int mt = (a.Cout + 63) / 64;
   const bool sw = a.relu == kActSwish;
-  if (nks == 1)
-    return sw ? launch_xp_cfg<1, true>(a, mt, stream) : launch_xp_cfg<1, false>(a, mt, stream);
-  if (nks == 2)
-    return sw ? launch_xp_cfg<2, true>(a, mt, stream) : launch_xp_cfg<2, false>(a, mt, stream);
+  if (nks == 1) return sw ? launch_xp_cfg<1, true>(a, stream) : launch_xp_cfg<1, false>(a, stream);
+  if (nks == 2) return sw ? launch_xp_cfg<2, true>(a, stream) : launch_xp_cfg<2, false>(a, stream);
   return hipErrorInvalidValue;
 }
 

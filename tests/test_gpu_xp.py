@@ -6,8 +6,8 @@ codes, int32 sums; for swish, which only the MFMA engines' epilogue has, the dir
 on every shape it accepts: MobileNet-V2 / EfficientNet-b0 expand shapes
 (input channels not a multiple of 64, one and two K-steps), partial Cout tiles, every
 epilogue form the fused executors use (ReLU6 codes, swish with the fp32 output, two code
-outputs, signed codes), and few persistent workgroups (TQ_XP_GRID) so each wave walks many
-pixel tiles."""
+outputs, signed codes), layers split into Cout groups, and few persistent workgroups per
+group (TQ_XP_GRID) so each wave walks many pixel tiles."""
 import pytest
 import torch
 import torch.nn as nn
@@ -59,8 +59,10 @@ def _run(x, lay, cout, hw, *, cfg, sc, sh, fmt, act, out, codes_b, kc_steps=0):
     (16, 96, 28, 3),     # MobileNet-V2 block 2 expand (Cp 16: one K-step, 48 zero codes)
     (24, 144, 14, 5),    # three Cout tiles, the last one 16 rows
     (40, 240, 9, 7),     # EfficientNet-b0 (P not a multiple of 32)
-    (64, 256, 7, 6),     # four Cout tiles (32 KB of weights, the limit)
+    (64, 256, 7, 6),     # four Cout tiles (32 KB of weights: one Cout group)
     (96, 100, 7, 3),     # two K-steps, partial Cout tile, pad code channels (cp 104)
+    (64, 384, 7, 4),     # two Cout groups of four tiles
+    (96, 576, 7, 3),     # two K-steps: five Cout groups of two tiles, the last one of one
 ])
 @pytest.mark.parametrize("form", ["relu6_codes", "swish_out", "two_codes", "signed"])
 @pytest.mark.parametrize("grid", ["0", "3"])
@@ -80,6 +82,7 @@ def test_xp_bit_identical_to_valu(cin, cout, hw, batch, form, grid, monkeypatch)
     else:
         ref = _run(x, lay_v, cout, hw, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
     monkeypatch.setenv("TQ_XP_GRID", grid)
+    monkeypatch.setenv("TQ_XP_GROUPS", "8")  # (the wide shapes: Cout groups)
     got = _run(x, lay_m, cout, hw, cfg=XP, sc=sc, sh=sh, fmt=torch.float16,
                kc_steps=lay_m.kc_steps, **kw)
     for g, r in zip(got, ref):
