@@ -16,9 +16,9 @@
 //     swizzled as the direct engine's, <= 32 KB: all of Cout, or MG groups of MT 64-row tiles
 //     for wider layers), the group's epilogue coefficients and the code tables once;
 //   * then each wave works alone (no barrier in the loop): a work item is 32 output pixels x
-//     every Cout tile of the group; its activation fragments (NKS x 4 x 16 bytes per lane) come straight
-//     from HBM into registers, and the NEXT item's are loaded before this item's MFMAs and
-//     epilogues run;
+//     every Cout tile of the group; its activation fragments (NKS x 4 x 16 bytes per lane)
+//     come straight from HBM into registers, and the NEXT item's are loaded before this
+//     item's MFMAs and epilogues run;
 //   * the epilogue reads the accumulators in the MFMA layout (lane = 4 consecutive channels
 //     of one pixel per quad), coefficients from LDS, no transpose: 8-byte code stores, one
 //     pixel's 2 Cout bytes written by one wave within the item.
@@ -61,8 +61,42 @@ void xp_groups(const ConvArgs& a, int nks, int* mt, int* mg) {
   *mg = (tiles + *mt - 1) / *mt;
 }
 
+// The fused executors' form of the expand convs -- ReLU / ReLU6 / swish (FAST = 1 / 2 / 3),
+// one code output served by its code table, no fp32 output -- with emit4_nhwc_res's
+// operations for that form only (fold, the activation the codes see, lut_codes' table path,
+// the store): the generic epilogue's runtime branches and stored value cost ~36 VALU per
+// output at ReLU6.
+template <int FAST>
+__device__ __forceinline__ void xp_emit_codes4(const ConvArgs& a, int64_t p, int co,
+                                               const int acc[4], const coef_t sc[4],
+                                               const coef_t sh[4], const uint16_t* lut) {
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    y[i] = fold_acc(acc[i], sc[i], sh[i]);
+    if (FAST == 3) {
+      y[i] = swish_f32(y[i]);
+    } else {
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (FAST == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;
+    }
+  }
+  uint32_t v[4];
+  if (FAST == 3) {
+    lut_codes<4>(y, a.inv_a, a.maxv_a, a.fmt_a, false, lut, v);  // signed values
+  } else {
+    uint32_t q[4];
+    relu_q_epi<4>(y, a.inv_a, a.maxv_a, q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = lut[q[i]];
+  }
+  int16_t* dst = a.codes_a + p * a.cp_a + co;
+  *reinterpret_cast<int2*>(dst) = make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+  if (co + 4 == a.Cout && a.cp_a > a.Cout) *reinterpret_cast<int2*>(dst + 4) = make_int2(0, 0);
+}
+
 // 5 waves per SIMD at one K-step (90 VGPRs, no spills; 6 spill), 4 at two
-template <int NKS, bool SWISH>
+template <int NKS, bool SWISH, int FAST>
 __global__ __launch_bounds__(kXpThreads) __attribute__((amdgpu_waves_per_eu(NKS == 1 ? 5 : 4)))
 void conv2d_tp_xp_kernel(ConvArgs a, int MT, int MG) {
   extern __shared__ __attribute__((aligned(16))) u32x4 xp_lds[];
@@ -161,7 +195,10 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT, int MG) {
             sc[e] = (coef_t)coef[2 * (co - mbase + e)];
             sh[e] = (coef_t)coef[2 * (co - mbase + e) + 1];
           }
-          emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, nores, lut_a, lut_b);
+          if constexpr (FAST != 0)
+            xp_emit_codes4<FAST>(a, p, co, acc4, sc, sh, lut_a);
+          else
+            emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, nores, lut_a, lut_b);
         }
       }
     }
@@ -172,12 +209,12 @@ void conv2d_tp_xp_kernel(ConvArgs a, int MT, int MG) {
   }
 }
 
-template <int NKS, bool SWISH>
+template <int NKS, bool SWISH, int FAST>
 hipError_t launch_xp_cfg(const ConvArgs& a, hipStream_t stream) {
   int mt, mg;
   xp_groups(a, NKS, &mt, &mg);
   const size_t lds = (size_t)xp_lds_bytes(a, NKS, mt);
-  const void* fn = reinterpret_cast<const void*>(&conv2d_tp_xp_kernel<NKS, SWISH>);
+  const void* fn = reinterpret_cast<const void*>(&conv2d_tp_xp_kernel<NKS, SWISH, FAST>);
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e =
@@ -198,7 +235,7 @@ hipError_t launch_xp_cfg(const ConvArgs& a, hipStream_t stream) {
   const int64_t need = (items + kXpThreads / 64 - 1) / (kXpThreads / 64);
   if (per_grp > need) per_grp = need;
   if (per_grp < 1) per_grp = 1;
-  conv2d_tp_xp_kernel<NKS, SWISH>
+  conv2d_tp_xp_kernel<NKS, SWISH, FAST>
       <<<dim3((unsigned)(per_grp * mg)), kXpThreads, lds, stream>>>(a, mt, mg);
   return hipGetLastError();
 }
@@ -219,11 +256,24 @@ bool conv_xp_eligible(const ConvArgs& a, int out_nhwc) {
   return mg <= xp_max_groups();
 }
 
+template <int NKS>
+hipError_t launch_xp_nks(const ConvArgs& a, hipStream_t stream) {
+  // (the two-K-step instantiations of the fast forms spill at 4 waves per SIMD)
+  const bool fast = NKS == 1 && a.out == nullptr && a.codes_a != nullptr &&
+                    a.codes_b == nullptr && a.lut_a > 0;
+  if constexpr (NKS == 1) {
+    if (fast && a.relu == kActSwish) return launch_xp_cfg<NKS, true, 3>(a, stream);
+    if (fast && a.relu == 2) return launch_xp_cfg<NKS, false, 2>(a, stream);
+    if (fast && a.relu == 1) return launch_xp_cfg<NKS, false, 1>(a, stream);
+  }
+  if (a.relu == kActSwish) return launch_xp_cfg<NKS, true, 0>(a, stream);
+  return launch_xp_cfg<NKS, false, 0>(a, stream);
+}
+
 hipError_t launch_conv2d_xp(const ConvArgs& a, hipStream_t stream) {
   const int nks = a.Kp / kKStep;
-  const bool sw = a.relu == kActSwish;
-  if (nks == 1) return sw ? launch_xp_cfg<1, true>(a, stream) : launch_xp_cfg<1, false>(a, stream);
-  if (nks == 2) return sw ? launch_xp_cfg<2, true>(a, stream) : launch_xp_cfg<2, false>(a, stream);
+  if (nks == 1) return launch_xp_nks<1>(a, stream);
+  if (nks == 2) return launch_xp_nks<2>(a, stream);
   return hipErrorInvalidValue;
 }
 

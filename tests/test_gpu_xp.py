@@ -64,7 +64,8 @@ def _run(x, lay, cout, hw, *, cfg, sc, sh, fmt, act, out, codes_b, kc_steps=0):
     (64, 384, 7, 4),     # two Cout groups of four tiles
     (96, 576, 7, 3),     # two K-steps: five Cout groups of two tiles, the last one of one
 ])
-@pytest.mark.parametrize("form", ["relu6_codes", "swish_out", "two_codes", "signed"])
+@pytest.mark.parametrize("form", ["relu6_codes", "relu_codes", "swish_codes", "swish_out",
+                                  "two_codes", "signed"])
 @pytest.mark.parametrize("grid", ["0", "3"])
 def test_xp_bit_identical_to_valu(cin, cout, hw, batch, form, grid, monkeypatch):
     lay_v, lay_m = _layers(cin, cout, monkeypatch, seed=cin + cout)
@@ -72,11 +73,13 @@ def test_xp_bit_identical_to_valu(cin, cout, hw, batch, form, grid, monkeypatch)
         memory_format=torch.channels_last)
     sc = (torch.rand(cout, dtype=torch.float64, device=DEV) + 0.5) * 2e-4
     sh = torch.randn(cout, dtype=torch.float64, device=DEV) * 0.1
-    kw = dict(relu6_codes=dict(act=6, out=False, codes_b=False),
+    kw = dict(relu6_codes=dict(act=6, out=False, codes_b=False),   # (the specialised forms)
+              relu_codes=dict(act=True, out=False, codes_b=False),
+              swish_codes=dict(act="swish", out=False, codes_b=False),
               swish_out=dict(act="swish", out=True, codes_b=False),
               two_codes=dict(act=True, out=True, codes_b=True),
               signed=dict(act=False, out=True, codes_b=False))[form]
-    if form == "swish_out":  # (the swish epilogue exists on the MFMA direct engine only)
+    if form.startswith("swish"):  # (the swish epilogue exists on the MFMA direct engine only)
         ref = _run(x, lay_m, cout, hw, cfg=DIRECT, sc=sc, sh=sh, fmt=torch.float16,
                    kc_steps=lay_m.kc_steps, **kw)
     else:
