@@ -45,7 +45,11 @@ __device__ __forceinline__ void dw_coef(const DwConvArgs& a, int c0, coef_t sc[C
   }
 }
 
-template <int CPL>
+// FAST: the fused executors' two forms with the generic path's operations for that form only
+// (its runtime branches and unused stored values cost VALU the kernel is short of):
+//   1 = ReLU / ReLU6 (a.relu), the next layer's codes from the table, no fp32 output, C == Cp
+//   2 = swish, fp32 output only (EfficientNet-b0: the squeeze-excite branch pools it)
+template <int CPL, int FAST = 0>
 __device__ __forceinline__ void dw_emit_coef(const DwConvArgs& a, const uint16_t* lut,
                                              int64_t p, int64_t img, int rem, int c0,
                                              const int acc[CPL], const coef_t sc[CPL],
@@ -54,6 +58,35 @@ __device__ __forceinline__ void dw_emit_coef(const DwConvArgs& a, const uint16_t
   float y[CPL];
 #pragma unroll
   for (int i = 0; i < CPL; ++i) y[i] = fold_acc(acc[i], sc[i], sh[i]);
+  if constexpr (FAST == 1) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+      if (a.relu == 2) y[i] = y[i] < 6.0f ? y[i] : 6.0f;
+    }
+    uint32_t qv[CPL], v[CPL];
+    relu_q_epi<CPL>(y, a.inv_c, a.maxv_c, qv);
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) v[i] = lut[qv[i]];
+    int16_t* dst = a.codes + p * a.cp_c + c0;
+    if (CPL == 4)
+      *reinterpret_cast<uint2*>(dst) =
+          make_uint2(v[0] | (v[1 % CPL] << 16), v[2 % CPL] | (v[3 % CPL] << 16));
+    else
+      *reinterpret_cast<uint32_t*>(dst) = v[0] | (v[1 % CPL] << 16);
+    return;
+  }
+  if constexpr (FAST == 2) {
+    float o[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) o[i] = swish_f32(y[i]);
+    float* dst = a.out + p * a.C + c0;
+    if (CPL == 4)
+      *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1 % CPL], o[2 % CPL], o[3 % CPL]);
+    else
+      *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1 % CPL]);
+    return;
+  }
   const bool full = (a.C % CPL) == 0;
   auto store_nhwc = [&](const float (&v)[CPL]) {
     float* dst = a.out + p * a.C + c0;  // NHWC (fused epilogue)
@@ -341,7 +374,7 @@ __global__ __launch_bounds__(256) void dwconv3_slide_kernel(DwConvArgs a) {
 // loads in flight for its whole segment instead of one load-then-compute shot, and the
 // weights and epilogue coefficients are loaded once per segment.  Same exact int32 sums and
 // epilogue as the other depthwise kernels (bit-identical outputs).
-template <int K, int S, int R, int CPL>
+template <int K, int S, int R, int CPL, int FAST = 0>
 __global__ __launch_bounds__(256) void dwconv_stream_kernel(DwConvArgs a, int seg) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lut[];  // next-layer code table
   if (a.lut_c) {
@@ -432,8 +465,8 @@ __global__ __launch_bounds__(256) void dwconv_stream_kernel(DwConvArgs a, int se
         }
       const int oh = oh0 + j;
       if (oh < oh_end)
-        dw_emit_coef<CPL>(a, l, (img * a.Ho + oh) * a.Wo + ow, img, oh * a.Wo + ow, c0, acc,
-                          sc, sh);
+        dw_emit_coef<CPL, FAST>(a, l, (img * a.Ho + oh) * a.Wo + ow, img, oh * a.Wo + ow, c0,
+                                acc, sc, sh);
     }
 #pragma unroll
     for (int k = 0; k < KEEP; ++k)
@@ -445,6 +478,20 @@ __global__ __launch_bounds__(256) void dwconv_stream_kernel(DwConvArgs a, int se
       for (int ks = 0; ks < K; ++ks) cur[KEEP + k][ks] = nxt[k][ks];
     ih0 += NEW;
   }
+}
+
+// One streaming-kernel shape with the epilogue form (dw_emit_coef FAST) the arguments allow.
+template <int K, int S, int R, int CPL>
+void launch_stream(const DwConvArgs& a, dim3 grid, size_t lds, int seg, hipStream_t stream) {
+  const bool fast1 = (a.relu == 1 || a.relu == 2) && a.out == nullptr && a.codes != nullptr &&
+                     a.lut_c > 0;
+  const bool fast2 = a.relu == kActSwish && a.out != nullptr && a.out_nhwc &&
+                     a.codes == nullptr && a.C % CPL == 0 && a.Cp == a.C;
+  const char* env = getenv("TQ_DW_FAST");  // 0: the generic epilogue (tests, A/B)
+  const bool on = !(env && atoi(env) == 0);
+  if (on && fast1) dwconv_stream_kernel<K, S, R, CPL, 1><<<grid, 256, lds, stream>>>(a, seg);
+  else if (on && fast2) dwconv_stream_kernel<K, S, R, CPL, 2><<<grid, 256, lds, stream>>>(a, seg);
+  else dwconv_stream_kernel<K, S, R, CPL, 0><<<grid, 256, lds, stream>>>(a, seg);
 }
 
 }  // namespace
@@ -496,17 +543,17 @@ hipError_t launch_dwconv_tp(const DwConvArgs& a, hipStream_t stream) {
     if (a.KH == 5) {
       // two channels per lane (4-byte loads): the 25 taps' weights of four channels would
       // take 100 VGPRs
-      if (S == 2) dwconv_stream_kernel<5, 2, 1, 2><<<grid, 256, lds, stream>>>(a, seg);
-      else if (R == 2) dwconv_stream_kernel<5, 1, 2, 2><<<grid, 256, lds, stream>>>(a, seg);
-      else dwconv_stream_kernel<5, 1, 1, 2><<<grid, 256, lds, stream>>>(a, seg);
+      if (S == 2) launch_stream<5, 2, 1, 2>(a, grid, lds, seg, stream);
+      else if (R == 2) launch_stream<5, 1, 2, 2>(a, grid, lds, seg, stream);
+      else launch_stream<5, 1, 1, 2>(a, grid, lds, seg, stream);
     } else if (S == 2) {
-      if (R == 1) dwconv_stream_kernel<3, 2, 1, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else if (R == 2) dwconv_stream_kernel<3, 2, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else dwconv_stream_kernel<3, 2, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
+      if (R == 1) launch_stream<3, 2, 1, 4>(a, grid, lds, seg, stream);
+      else if (R == 2) launch_stream<3, 2, 2, 4>(a, grid, lds, seg, stream);
+      else launch_stream<3, 2, 4, 4>(a, grid, lds, seg, stream);
     } else {
-      if (R == 2) dwconv_stream_kernel<3, 1, 2, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else if (R == 4) dwconv_stream_kernel<3, 1, 4, 4><<<grid, 256, lds, stream>>>(a, seg);
-      else dwconv_stream_kernel<3, 1, 8, 4><<<grid, 256, lds, stream>>>(a, seg);
+      if (R == 2) launch_stream<3, 1, 2, 4>(a, grid, lds, seg, stream);
+      else if (R == 4) launch_stream<3, 1, 4, 4>(a, grid, lds, seg, stream);
+      else launch_stream<3, 1, 8, 4>(a, grid, lds, seg, stream);
     }
     return hipGetLastError();
   }

@@ -265,3 +265,45 @@ def test_dw5_streaming_kernel_bit_identical(cfg, relu, monkeypatch):
     for o, nc in outs[1:]:
         assert torch.equal(o, outs[0][0]) and torch.equal(nc, outs[0][1])
     assert not torch.isnan(outs[0][0].view(torch.float32)).any()
+
+
+@pytest.mark.parametrize("cfg", [
+    # c, k, hw, stride, (pad top, pad left), ho: MobileNet-V2 / EfficientNet-b0 shapes, pad
+    # channels (c 20 -> cp 24), static-same stride 2
+    (32, 3, 14, 1, (1, 1), 14), (144, 3, 28, 2, (1, 1), 14), (20, 3, 9, 1, (1, 1), 9),
+    (40, 5, 28, 1, (2, 2), 28), (240, 5, 28, 2, (1, 1), 14), (20, 5, 9, 1, (2, 2), 9),
+])
+@pytest.mark.parametrize("form", ["relu6_codes", "relu_codes", "swish_out"])
+def test_dw_fast_epilogue_bit_identical(cfg, form, monkeypatch):
+    """The streaming depthwise kernel's specialised epilogues (dw_emit_coef FAST: ReLU / ReLU6
+    with table codes only, swish with the fp32 output only -- the fused executors' forms)
+    against its generic epilogue (TQ_DW_FAST=0): bit-identical codes / outputs."""
+    import tq_native
+    c, k, hw, s, (pt, pl), ho = cfg
+    torch.manual_seed(c + hw + k)
+    conv = nn.Conv2d(c, c, k, s, k // 2, groups=c, bias=False)
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 16, 1, 16)
+    cp = layer.act_channels
+    x = torch.relu(torch.randn(3, c, hw, hw, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.zeros((3, hw, hw, cp), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, codes)
+    sc = torch.rand(c, dtype=torch.float64, device=DEV) * 1e-5
+    sh = torch.randn(c, dtype=torch.float64, device=DEV) * 0.1
+    act = {"relu6_codes": 6, "relu_codes": True, "swish_out": "swish"}[form]
+    outs = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("TQ_DW_FAST", fast)
+        o = nc = None
+        if form == "swish_out":
+            o = torch.full((3, c, ho, ho), float("nan"), device=DEV).contiguous(
+                memory_format=torch.channels_last)
+        else:
+            nc = torch.full((3, ho, ho, cp), -1, dtype=torch.int16, device=DEV)
+        tq_native.dwconv2d_termpair_fused(codes, c, layer.w_codes, k, k, (s, s), (pt, pl),
+                                          (1, 1), ho, ho, sc, sh, act, out=o, next_codes=nc,
+                                          quant=(0.03, 9, 3))
+        outs.append(o.view(torch.int32).cpu() if o is not None else nc.cpu())
+    assert torch.equal(outs[0], outs[1])
+    if form != "swish_out":
+        assert (outs[0] != -1).all()  # every code written, pad channels included
