@@ -99,6 +99,43 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
                                SWISH ? false : (bool)a.relu, lut_b);
 }
 
+// emit4_nhwc_res for the ResNet executors' form -- ReLU, the code outputs served by their
+// tables (a.lut_a, and a.lut_b when codes_b) -- with that form's operations only: the same
+// values and stores without the runtime branches (and registers) of the other forms'.
+__device__ __forceinline__ void emit4_relu_lut(const ConvArgs& a, int64_t p, int co,
+                                               const int acc[4], const coef_t sc[4],
+                                               const coef_t sh[4], const float4 rv,
+                                               const uint16_t* lut_a, const uint16_t* lut_b) {
+  const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+  float y[4], o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    y[i] = fold_acc(acc[i], sc[i], sh[i]);
+    if (a.residual || a.ds_x) y[i] += r[i];
+    o[i] = y[i];
+    y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+    o[i] = o[i] != o[i] ? o[i] : y[i];
+  }
+  if (a.out)
+    *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    int16_t* codes = side ? a.codes_b : a.codes_a;
+    if (side && !codes) break;
+    const int cp = side ? a.cp_b : a.cp_a;
+    const uint16_t* lut = side ? lut_b : lut_a;
+    uint32_t q[4];
+    relu_q_epi<4>(y, side ? a.inv_b : a.inv_a, side ? a.maxv_b : a.maxv_a, q);
+    uint32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = lut[q[i]];
+    *reinterpret_cast<int2*>(codes + p * cp + co) =
+        make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+    if (co + 4 == a.Cout && cp > a.Cout)
+      *reinterpret_cast<int2*>(codes + p * cp + co + 4) = make_int2(0, 0);
+  }
+}
+
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:
 // one fp64->fp32 rounding, residual add and ReLU in fp32, fp32 store, next layers' TR codes
 // (tr_layer.py:96-99 applied to the stored value).

@@ -77,7 +77,8 @@ struct DirCfg {
 // main conv's, into fresh fp32 accumulators, while the main conv's sums wait in int32; the
 // epilogue turns them into the identity (what the separate downsample conv would store) and
 // adds it where a residual read from HBM would go.
-template <int MB, bool FLUSH, bool DS, bool SWISH>
+// EPI 1: the epilogue of the ReLU + code-table form only (emit4_relu_lut; the host picks it)
+template <int MB, bool FLUSH, bool DS, bool SWISH, int EPI = 0>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
   constexpr int NBM = 2 * MB;  // 32-row MFMA blocks per wave
@@ -422,7 +423,10 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
                             : make_float4(0.f, 0.f, 0.f, 0.f);
       const u32x4 v = t[px * C::SL + (sl ^ (px & 15))];
       const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-      emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
+      if constexpr (EPI == 1)
+        emit4_relu_lut(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
+      else
+        emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
     }
 #if !TQ_PHASE_TRACE
     return;
@@ -451,7 +455,9 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
     if (acc4[0] == 0x7fffffff && a.out) a.out[p] = res[it].x + (float)(sc[0] + sh[0]);
     continue;
 #endif
-    if (vec)
+    if constexpr (EPI == 1)
+      emit4_relu_lut(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);  // (host: vec)
+    else if (vec)
       emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
       emit4_nhwc(a, p, co, acc4, sc, sh, false, lut_a, lut_b);
@@ -660,27 +666,37 @@ hipError_t launch_pw_cfg(const ConvArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <int MB, bool FLUSH, bool DS, bool SWISH = false>
+template <int MB, bool FLUSH, bool DS, bool SWISH = false, int EPI = 0>
 hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   using C = DirCfg<MB>;
   const int64_t tiles = ((a.P + C::BN - 1) / C::BN) * ((a.Cout + C::BM - 1) / C::BM);
   static bool attr_set = false;  // the MB = 2 ring + code tables pass the 64 KB default
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH>),
+        reinterpret_cast<const void*>(&conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH, EPI>),
         hipFuncAttributeMaxDynamicSharedMemorySize,
         160 * 1024 - (C::BM + (DS ? C::BM : 1)) * 16);  // minus the static coef arrays
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH>
+  conv2d_tp_direct_kernel<MB, FLUSH, DS, SWISH, EPI>
       <<<dim3((unsigned)tiles), kDirThreads, (size_t)(C::LDS * 16 + conv_lut_bytes(a)), stream>>>(a);
   return hipGetLastError();
+}
+
+// The ReLU + code-table form of the fused executors' convs (emit4_relu_lut).
+bool direct_relu_lut_form(const ConvArgs& a) {
+  const char* env = getenv("TQ_EPI_FAST");  // 0: the generic epilogue (tests, A/B)
+  return !(env && atoi(env) == 0) && a.relu == 1 && a.codes_a != nullptr && a.lut_a > 0 &&
+         (a.codes_b == nullptr || a.lut_b > 0) && (a.Cout & 3) == 0;
 }
 
 template <int MB, bool DS>
 hipError_t launch_direct_mb(const ConvArgs& a, hipStream_t stream) {
   const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
+  if (MB == 1 && !DS && direct_relu_lut_form(a))
+    return flush ? launch_direct_cfg<1, true, false, false, 1>(a, stream)
+                 : launch_direct_cfg<1, false, false, false, 1>(a, stream);
   return flush ? launch_direct_cfg<MB, true, DS>(a, stream)
                : launch_direct_cfg<MB, false, DS>(a, stream);
 }

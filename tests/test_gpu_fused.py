@@ -427,3 +427,26 @@ def test_act_encode_act_code_table_bit_identical(act, gated, fmt, monkeypatch):
     ref = torch.from_numpy(oracle.tr(v.numpy(), 0.05, 9, 1, 3)) / 0.05
     assert torch.equal(res[0][0][..., :c], ref.round())
     assert (res[0][0][..., c:] == 0).all()
+
+
+def test_fused_resnet_specialised_epilogues_bit_identical(monkeypatch):
+    """The engines' epilogues specialised to the executor's ReLU + code-table form (direct
+    engine emit4_relu_lut, TQ_EPI_FAST) give the generic epilogue's bits: every captured conv
+    output and code, and the logits."""
+    torch.manual_seed(2)
+    model = cnn_models.resnet18(pretrained=False).to(DEV).eval()
+    settings = cnn_models.static_conv_layer_settings(model, 9, 8, 12)
+    q = cnn_models.convert_model(model, settings, 9, 3).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        q(x)
+    tr_layer.set_tr_tracking(q, False)
+    fused = tq_fuse.FusedResNet(q)
+    runs = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("TQ_EPI_FAST", fast)
+        with torch.no_grad():
+            logits = fused(x)  # (bench mode: no fp32 outputs the executor does not need)
+        torch.cuda.synchronize()
+        runs.append(logits.view(torch.int32).cpu())
+    assert torch.equal(runs[0], runs[1])
