@@ -98,8 +98,10 @@ struct StripEpi {
 // in a dummy slot.  A fixed count keeps the compiler's vmcnt bookkeeping exact.
 constexpr int kStripDma = ((kStripTR + 2) * kStripMaxW * 8 / 64 + 3) / 4;
 
-// The epilogue of 4 consecutive tile pixels P0 .. P0 + 3 of this lane's channel.
-template <bool RES, bool OUT, bool CB, bool FULL>
+// The epilogue of 4 consecutive tile pixels P0 .. P0 + 3 of this lane's channel.  LUT: the
+// fused executor's form only -- ReLU, every code output from its table (the host checks) --
+// without the computed-code paths and the runtime activation branches.
+template <bool RES, bool OUT, bool CB, bool FULL, bool LUT>
 __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& ep,
                                             const float acc4[4], const float rv[4], int P0,
                                             int nvalid, float* outp, int16_t* ca, int16_t* cbp,
@@ -110,9 +112,9 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
     y[e] = fold_acc((int)acc4[e], (coef_t)ep.sc, (coef_t)ep.sh);
     if (RES) y[e] += rv[e];  // (no + 0.0f without one: -0.0 stays, as in tq_epilogue.h)
     o[e] = y[e];
-    if (a.relu) {
+    if (LUT || a.relu) {
       y[e] = y[e] > 0.0f ? y[e] : 0.0f;
-      if (a.relu == 2) y[e] = y[e] < 6.0f ? y[e] : 6.0f;  // ReLU6
+      if (!LUT && a.relu == 2) y[e] = y[e] < 6.0f ? y[e] : 6.0f;  // ReLU6
       o[e] = o[e] != o[e] ? o[e] : y[e];  // the stored value keeps a NaN (torch.relu)
     }
   }
@@ -133,12 +135,12 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
     // the code table after a ReLU only: the signed-value variant (tq_device.h lut_codes) put
     // this engine over its register budget (scratch spills: 127 -> 177 us, r03ai); without a
     // ReLU the codes are computed
-    if (lut && act_nonneg(a.relu)) {
+    if (LUT || (lut && act_nonneg(a.relu))) {
       uint32_t qv[4];
       relu_q_epi<4>(y, inv, maxv, qv);
 #pragma unroll
       for (int e = 0; e < 4; ++e) bits[e] = lut[qv[e]];
-    } else {
+    } else if constexpr (!LUT) {
       int32_t v[4];
       if (side ? ep.fast_b : ep.fast_a) {
         tr_values_relu4(y, inv, maxv, side ? ep.npeel_b : ep.npeel_a, v);
@@ -160,7 +162,7 @@ __device__ __forceinline__ void strip_emit4(const ConvArgs& a, const StripEpi& e
 // RES / OUT / CB: residual input, fp32 output, second code target present (compile-time, so
 // each instantiation carries only the epilogue it runs).  `refill` runs after the epilogue
 // (team sync + the next patch's DMA, which then lands during the next tile's sync wait).
-template <int NB, bool RES, bool OUT, bool CB, typename Refill>
+template <int NB, bool RES, bool OUT, bool CB, bool LUT, typename Refill>
 __device__ __forceinline__ void strip_tile(const ConvArgs& a, const u32x4* patch,
                                            const u32x4* wrow_ptr, int wkey, int W, int ZP,
                                            int pset, int r32, int hh, int co, int64_t pix0,
@@ -271,11 +273,11 @@ __device__ __forceinline__ void strip_tile(const ConvArgs& a, const u32x4* patch
       if (RES) load_res(g, rv4);  // latency covered by the other team's waves
       __builtin_amdgcn_sched_barrier(0);  // one group's loads and values live at a time
       if (full)
-        strip_emit4<RES, OUT, CB, true>(a, ep, acc4, rv4, pl + 8 * q, nvalid, outp + off,
+        strip_emit4<RES, OUT, CB, true, LUT>(a, ep, acc4, rv4, pl + 8 * q, nvalid, outp + off,
                                    ca ? ca + off : nullptr, cbp ? cbp + off : nullptr, lut_a,
                                    lut_b);
       else
-        strip_emit4<RES, OUT, CB, false>(a, ep, acc4, rv4, pl + 8 * q, nvalid, outp + off,
+        strip_emit4<RES, OUT, CB, false, LUT>(a, ep, acc4, rv4, pl + 8 * q, nvalid, outp + off,
                                     ca ? ca + off : nullptr, cbp ? cbp + off : nullptr, lut_a,
                                     lut_b);
     }
@@ -283,7 +285,7 @@ __device__ __forceinline__ void strip_tile(const ConvArgs& a, const u32x4* patch
   refill();
 }
 
-template <bool RES, bool OUT, bool CB>
+template <bool RES, bool OUT, bool CB, bool LUT>
 __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvArgs a,
                                                                            int64_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
@@ -410,13 +412,13 @@ __global__ __launch_bounds__(kStripThreads, 2) void conv2d_tp_strip_kernel(ConvA
     asm volatile("" : "+v"(r32), "+v"(hh));
     const int co = 32 * cb + r32;
     switch (nb) {  // wave-uniform
-      case 4: strip_tile<4, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
+      case 4: strip_tile<4, RES, OUT, CB, LUT>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
                                           pix0, nv, ep, refill, lut_a, lut_b); break;
-      case 3: strip_tile<3, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
+      case 3: strip_tile<3, RES, OUT, CB, LUT>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
                                           pix0, nv, ep, refill, lut_a, lut_b); break;
-      case 2: strip_tile<2, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
+      case 2: strip_tile<2, RES, OUT, CB, LUT>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
                                           pix0, nv, ep, refill, lut_a, lut_b); break;
-      case 1: strip_tile<1, RES, OUT, CB>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
+      case 1: strip_tile<1, RES, OUT, CB, LUT>(a, patch, wrow_ptr, wkey, W, ZP, pset, r32, hh, co,
                                           pix0, nv, ep, refill, lut_a, lut_b); break;
       default: refill(); break;
     }
@@ -445,16 +447,24 @@ bool conv_strip_eligible(const ConvArgs& a, int out_nhwc) {
          (a.residual == nullptr || strip_res_ok()) && a.ds_x == nullptr;
 }
 
-template <bool RES, bool OUT, bool CB>
-hipError_t launch_strip_mode(const ConvArgs& a, hipStream_t stream) {
+template <bool RES, bool OUT, bool CB, bool LUT>
+hipError_t launch_strip_lut(const ConvArgs& b, int64_t grid, int64_t bytes, int64_t ntiles,
+                            hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv2d_tp_strip_kernel<RES, OUT, CB>),
+        reinterpret_cast<const void*>(&conv2d_tp_strip_kernel<RES, OUT, CB, LUT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  conv2d_tp_strip_kernel<RES, OUT, CB, LUT><<<dim3((unsigned)grid), kStripThreads,
+                                               (size_t)bytes, stream>>>(b, ntiles);
+  return hipGetLastError();
+}
+
+template <bool RES, bool OUT, bool CB>
+hipError_t launch_strip_mode(const ConvArgs& a, hipStream_t stream) {
   const int64_t ntiles = (int64_t)a.N * ((a.Ho + kStripTR - 1) / kStripTR);
   int64_t grid = device_cus();
   if (grid > ntiles) grid = ntiles;
@@ -464,9 +474,13 @@ hipError_t launch_strip_mode(const ConvArgs& a, hipStream_t stream) {
     b.lut_a = b.lut_b = 0;
     bytes = strip_lds_bytes(a.W);
   }
-  conv2d_tp_strip_kernel<RES, OUT, CB><<<dim3((unsigned)grid), kStripThreads, (size_t)bytes,
-                                          stream>>>(b, ntiles);
-  return hipGetLastError();
+  // the fused executor's form (ReLU, table codes): the LUT-only epilogue (TQ_EPI_FAST=0: the
+  // generic one)
+  const char* env = getenv("TQ_EPI_FAST");
+  const bool lut = !(env && atoi(env) == 0) && b.relu == 1 && b.codes_a != nullptr &&
+                   b.lut_a > 0 && (b.codes_b == nullptr || b.lut_b > 0);
+  return lut ? launch_strip_lut<RES, OUT, CB, true>(b, grid, bytes, ntiles, stream)
+             : launch_strip_lut<RES, OUT, CB, false>(b, grid, bytes, ntiles, stream);
 }
 
 hipError_t strip_sync_faults(uint32_t* count) {
