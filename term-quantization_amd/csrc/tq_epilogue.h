@@ -9,6 +9,8 @@
 //   into the stored value as torch.relu does; the codes of a NaN are 0, as TR(NaN) = 0.
 #pragma once
 
+#include <stdlib.h>
+
 #include "tq_device.h"
 #include "tq_launch.h"
 
@@ -134,6 +136,28 @@ __device__ __forceinline__ void emit4_relu_lut(const ConvArgs& a, int64_t p, int
     if (co + 4 == a.Cout && cp > a.Cout)
       *reinterpret_cast<int2*>(codes + p * cp + co + 4) = make_int2(0, 0);
   }
+}
+
+// The identity form (a downsample conv: no activation, no residual, no codes, fp32 output
+// only) of emit4_nhwc_res: the fold and the store.
+__device__ __forceinline__ void emit4_identity(const ConvArgs& a, int64_t p, int co,
+                                               const int acc[4], const coef_t sc[4],
+                                               const coef_t sh[4]) {
+  *reinterpret_cast<float4*>(a.out + p * a.Cout + co) =
+      make_float4(fold_acc(acc[0], sc[0], sh[0]), fold_acc(acc[1], sc[1], sh[1]),
+                  fold_acc(acc[2], sc[2], sh[2]), fold_acc(acc[3], sc[3], sh[3]));
+}
+
+// Epilogue form of a conv launch the engines specialise (0 = the generic emit4_nhwc(_res)):
+// 1 = ReLU with every code output from its table (emit4_relu_lut), 2 = the identity form
+// (emit4_identity).  TQ_EPI_FAST=0 keeps the generic epilogue (tests, A/B).
+__host__ inline int epilogue_form(const ConvArgs& a) {
+  const char* env = getenv("TQ_EPI_FAST");
+  if ((env && atoi(env) == 0) || (a.Cout & 3) || a.ds_x) return 0;
+  if (a.relu == 1 && a.codes_a && a.lut_a > 0 && (a.codes_b == nullptr || a.lut_b > 0))
+    return 1;
+  if (a.relu == 0 && a.out && !a.codes_a && !a.codes_b && !a.residual) return 2;
+  return 0;
 }
 
 // Finish channels co..co+3 of output pixel p (channels_last) from exact integer sums:

@@ -77,7 +77,7 @@ struct DirCfg {
 // main conv's, into fresh fp32 accumulators, while the main conv's sums wait in int32; the
 // epilogue turns them into the identity (what the separate downsample conv would store) and
 // adds it where a residual read from HBM would go.
-// EPI 1: the epilogue of the ReLU + code-table form only (emit4_relu_lut; the host picks it)
+// EPI: tq_epilogue.h epilogue_form (1 ReLU + code tables, 2 identity; the host picks it)
 template <int MB, bool FLUSH, bool DS, bool SWISH, int EPI = 0>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
@@ -425,6 +425,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
       const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
       if constexpr (EPI == 1)
         emit4_relu_lut(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
+      else if constexpr (EPI == 2)
+        emit4_identity(a, p, c4, acc4, psc, psh);
       else
         emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
     }
@@ -457,6 +459,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
 #endif
     if constexpr (EPI == 1)
       emit4_relu_lut(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);  // (host: vec)
+    else if constexpr (EPI == 2)
+      emit4_identity(a, p, co, acc4, sc, sh);
     else if (vec)
       emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
@@ -684,19 +688,16 @@ hipError_t launch_direct_cfg(const ConvArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// The ReLU + code-table form of the fused executors' convs (emit4_relu_lut).
-bool direct_relu_lut_form(const ConvArgs& a) {
-  const char* env = getenv("TQ_EPI_FAST");  // 0: the generic epilogue (tests, A/B)
-  return !(env && atoi(env) == 0) && a.relu == 1 && a.codes_a != nullptr && a.lut_a > 0 &&
-         (a.codes_b == nullptr || a.lut_b > 0) && (a.Cout & 3) == 0;
-}
-
 template <int MB, bool DS>
 hipError_t launch_direct_mb(const ConvArgs& a, hipStream_t stream) {
   const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
-  if (MB == 1 && !DS && direct_relu_lut_form(a))
+  const int form = MB == 1 && !DS ? epilogue_form(a) : 0;
+  if (form == 1)
     return flush ? launch_direct_cfg<1, true, false, false, 1>(a, stream)
                  : launch_direct_cfg<1, false, false, false, 1>(a, stream);
+  if (form == 2)
+    return flush ? launch_direct_cfg<1, true, false, false, 2>(a, stream)
+                 : launch_direct_cfg<1, false, false, false, 2>(a, stream);
   return flush ? launch_direct_cfg<MB, true, DS>(a, stream)
                : launch_direct_cfg<MB, false, DS>(a, stream);
 }

@@ -269,7 +269,7 @@ struct PipeCfg {
   static_assert(LPW * (NS - 2) <= 63, "vmcnt range");
 };
 
-template <int BM, int BN, int NS, bool OUT_NHWC>
+template <int BM, int BN, int NS, bool OUT_NHWC, int EPI = 0>
 __global__ __launch_bounds__(pipe_threads(BM, BN), 1) void conv2d_tp_mfma_pipe_kernel(
     ConvArgs a) {
   using C = PipeCfg<BM, BN, NS>;
@@ -432,9 +432,29 @@ __global__ __launch_bounds__(pipe_threads(BM, BN), 1) void conv2d_tp_mfma_pipe_k
       if (p >= a.P) continue;
       const u32x4 v = t[px * 16 + (slot ^ (px & 15))];
       const int acc4[4] = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-      emit4_nhwc(a, p, co, acc4, sc, sh, vec, lut_a, lut_b);
+      if constexpr (EPI == 1)  // (epilogue_form 1 without a residual)
+        emit4_relu_lut(a, p, co, acc4, sc, sh, make_float4(0.f, 0.f, 0.f, 0.f), lut_a, lut_b);
+      else if constexpr (EPI == 2)
+        emit4_identity(a, p, co, acc4, sc, sh);
+      else
+        emit4_nhwc(a, p, co, acc4, sc, sh, vec, lut_a, lut_b);
     }
   }
+}
+
+template <int BM, int BN, int NS, int EPI>
+hipError_t launch_pipe_nhwc(const ConvArgs& b, dim3 grid, size_t dyn, hipStream_t stream) {
+  using C = PipeCfg<BM, BN, NS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true, EPI>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kLutMax * 2);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true, EPI><<<grid, C::THREADS, dyn, stream>>>(b);
+  return hipGetLastError();
 }
 
 template <int BM, int BN, int NS>
@@ -444,21 +464,18 @@ hipError_t launch_pipe_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
   const dim3 grid((unsigned)tiles);
   ConvArgs b = a;
   if ((int64_t)C::LDS * 16 + conv_lut_bytes(b) > 160 * 1024) b.lut_a = b.lut_b = 0;
-  const size_t dyn = out_nhwc ? (size_t)conv_lut_bytes(b) : 0;
-  if (!out_nhwc) b.lut_a = b.lut_b = 0;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kLutMax * 2);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  if (out_nhwc)
-    conv2d_tp_mfma_pipe_kernel<BM, BN, NS, true><<<grid, C::THREADS, dyn, stream>>>(b);
-  else
+  if (!out_nhwc) {
+    b.lut_a = b.lut_b = 0;
     conv2d_tp_mfma_pipe_kernel<BM, BN, NS, false><<<grid, C::THREADS, 0, stream>>>(b);
-  return hipGetLastError();
+    return hipGetLastError();
+  }
+  const size_t dyn = (size_t)conv_lut_bytes(b);
+  // the specialised epilogues (the ReLU one without a residual: the generic path loads it)
+  const int form = epilogue_form(b);
+  if (form == 1 && b.residual == nullptr)
+    return launch_pipe_nhwc<BM, BN, NS, 1>(b, grid, dyn, stream);
+  if (form == 2) return launch_pipe_nhwc<BM, BN, NS, 2>(b, grid, dyn, stream);
+  return launch_pipe_nhwc<BM, BN, NS, 0>(b, grid, dyn, stream);
 }
 
 template <int BM, int BN>
