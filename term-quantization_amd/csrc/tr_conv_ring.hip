@@ -37,6 +37,8 @@
 //               [Cout][2] fp64 epilogue coefficients | epilogue code tables
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "tq_device.h"
 #include "tq_epilogue.h"
 #include "tq_launch.h"
@@ -138,6 +140,30 @@ __host__ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// Stream-K tail (SK kernels).  The q full rounds of tiles (tiles [0, q G), one per workgroup
+// and round) run data-parallel as in the plain kernel; the remaining tiles -- the partial last
+// round, which would leave most CUs idle -- become a chunk-granular unit stream, unit =
+// (tile - q G) * nch + chunk, and workgroup g takes the units [g U / G, (g + 1) U / G).  A tile
+// split over workgroups is finished by whichever contributor arrives last: every contributor
+// stores its int32 partial sums write-through (sc1) into its own slab, drains, and draws a
+// ticket from the tile's counter (indexed by the workgroup owning the tile's first unit); the
+// last one adds the other slabs (sc1 loads) to its registers and runs the epilogue.  Integer
+// partial sums add exactly in any order, so the output is the one of the unsplit tile.  The
+// last arriver resets the counter (zeroed once at allocation), and nothing ever waits on
+// another workgroup.
+struct RingSk {
+  int* cnt;     // [G] tile tickets
+  int* slab;    // [G][2][64 * NW * 64] int32 partial sums: slot 0 the range's first tile,
+                // slot 1 its last one
+  int64_t U;    // units in the split tail
+  int64_t q;    // full data-parallel rounds ahead of the tail: tiles [0, q G)
+};
+
+// workgroup owning unit u: the g with floor(g U / G) <= u < floor((g + 1) U / G)
+__device__ __forceinline__ int sk_owner(int64_t u, int64_t U, int64_t G) {
+  return (int)(((u + 1) * G + U - 1) / U - 1);
+}
+
 __device__ __forceinline__ half8 lds_frag(uint32_t byte_addr) {
   if (RING_AB == 7) return (half8)(_Float16)(byte_addr & 7);  // timing only: no LDS reads
   return __builtin_bit_cast(
@@ -148,9 +174,9 @@ __device__ __forceinline__ half8 lds_frag(uint32_t byte_addr) {
 // FAST: the fused ResNet executor's epilogue form, specialised at launch -- ReLU, fp16 codes
 // from the code tables (every code output has one), Cout % 4 == 0 -- with per-pixel base
 // pointers and compile-time channel offsets; other forms run the shared emit4_nhwc_res.
-template <int NW, int KS, int PI, bool FLUSH, bool FAST>
+template <int NW, int KS, int PI, bool FLUSH, bool FAST, bool SK>
 __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, int R,
-                                                                   int64_t ptc) {
+                                                                   int64_t ptc, RingSk sk) {
   using Gm = RingGeom<NW, KS>;
   constexpr int NR = Gm::slots(PI);
   constexpr int WI = Gm::WI, CH = Gm::CH, SH = Gm::SH, SUB = Gm::SUB;
@@ -281,18 +307,44 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
   if (blockIdx.x & 1)
     for (int i = 0; i < a.ab; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
-  // ---- the tile stream
-  int64_t tile = g;
+  // ---- this workgroup's tile sequence, j = 0, 1, ...: first the data-parallel tiles g + j G
+  // (all of them without SK; SK: the sk.q full rounds), then (SK) the tiles its range of the
+  // tail's units [u0, u1) meets -- the first one from chunk u0 % nch, the last one up to
+  // chunk (u1 - 1) % nch
+  const int64_t dp_n = SK ? sk.q : (T - g + G - 1) / G;
+  int64_t u0 = 0, u1 = 0, sk_first = 0, n_sk = 0;
+  if constexpr (SK) {
+    u0 = g * sk.U / G;
+    u1 = (g + 1) * sk.U / G;
+    if (u1 > u0) {
+      sk_first = sk.q * G + u0 / nch;
+      n_sk = sk.q * G + (u1 - 1) / nch - sk_first + 1;
+    }
+  }
+  const int64_t n_seq = dp_n + n_sk;
+  if (n_seq == 0) return;  // (uniform: the whole workgroup leaves before any barrier)
+  auto tile_at = [&](int64_t j) __attribute__((always_inline)) {
+    return j < dp_n ? g + j * G : sk_first + (j - dp_n);
+  };
+  auto chunk_lo = [&](int64_t j) __attribute__((always_inline)) {
+    return SK && j == dp_n ? (int)(u0 % nch) : 0;
+  };
+  auto chunk_hi = [&](int64_t j) __attribute__((always_inline)) {
+    return SK && j >= dp_n && j == n_seq - 1 ? (int)((u1 - 1) % nch) + 1 : nch;
+  };
+  int64_t seq = 0;
+  int64_t tile = tile_at(0);
   RingTile cur = ring_tile(a, tile, R, mt, a.m_slow, ptc);
-  int64_t ntile = tile + G;
-  RingTile nxt = ring_tile(a, ntile < T ? ntile : tile, R, mt, a.m_slow, ptc);
+  RingTile nxt = ring_tile(a, tile_at(seq + 1 < n_seq ? seq + 1 : seq), R, mt, a.m_slow, ptc);
   setup_b(cur);
-  // prologue: chunk 0's patch into buffer 0, weight images of steps 0 .. NR-2
+  int c_lo = chunk_lo(0), c_hi = chunk_hi(0);
+  // prologue: chunk c_lo's patch into buffer 0, weight images of steps 0 .. NR-2
 #pragma unroll
   for (int j = 0; j < PI; ++j)
-    issue_piece(j, reinterpret_cast<const char*>(xg + cur.base * a.W * a.Cp), cur.px, 0);
+    issue_piece(j, reinterpret_cast<const char*>(xg + cur.base * a.W * a.Cp + (int64_t)c_lo * KS),
+                cur.px, 0);
 #pragma unroll
-  for (int j = 0; j + 1 < NR; ++j) issue_w(cur.m0, j, 0, j, true);
+  for (int j = 0; j + 1 < NR; ++j) issue_w(cur.m0, j, c_lo, j, true);
   TQ_WAIT_VM(0);
   __syncthreads();  // coefficients, tables, zero pixel, the first images visible
   // ring slot of the current chunk's tap 0 (the stream's step index mod NR; 0 when NR | 9)
@@ -345,13 +397,13 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
           accf[bm][bn][r] = 0.0f;
           if (FLUSH) acci[bm][bn][r] = 0;
         }
-    const bool has_next = ntile < T;
+    const bool has_next = seq + 1 < n_seq;
     int since = 0;
-    for (int c = 0; c < nch; ++c) {
-      const bool last_chunk = c + 1 == nch;
+    for (int c = c_lo; c < c_hi; ++c) {
+      const bool last_chunk = c + 1 == c_hi;
       // the chunk after this one in the stream: its patch rows, channel chunk and weights
       const int64_t nbase = last_chunk ? nxt.base : cur.base;
-      const int nc = last_chunk ? 0 : c + 1;
+      const int nc = last_chunk ? chunk_lo(seq + 1) : c + 1;  // (a tail tile may start mid-tile)
       const int nm0 = last_chunk ? nxt.m0 : cur.m0;
       const bool nlive = !last_chunk || has_next;
       const int npx = nlive ? (last_chunk ? nxt.px : cur.px) : 0;  // 0: every lane reads zeros
@@ -458,129 +510,199 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
       sbase = (sbase + kRingTaps) % NR;
     }
 
-    // ---- epilogue from the MFMA layout: lane (r32, hh) of block (bm, bn) holds channels
-    // m0 + wm + 32 bm + 8 q + 4 hh + [0, 4) of pixel column wn + 32 bn + r32
-    if constexpr (FAST) {
-      const int cl = cur.m0 + wm + 4 * hh;  // the lane's first channel
-      const double* cf = coef + 2 * cl;
-      // one pixel block's residual loads at a time (FLUSH: both blocks' would spill)
-      float4 rv_next[2][4];
-      static_for<0, 2>([&](auto bnc) __attribute__((always_inline)) {
-        constexpr int bn = decltype(bnc)::value;
-        const int j = wn + 32 * bn + r32;
-        const int64_t p = cur.p0 + j;
-        const bool okp = j < BNv && p < a.P;
-        const int64_t pc = okp ? p * a.Cout + cl : 0;
-        float4 rv[2][4];
-        if constexpr (FLUSH) {
-          load_res(cur, bn, rv);
-        } else if constexpr (bn == 0) {
-          load_res(cur, 1, rv_next);  // block 1's loads in flight during block 0
+    // ---- a split tile (SK): partial sums to this workgroup's slab; the last contributor adds
+    // the others' and runs the epilogue (RingSk)
+    bool emit = true;
+    if constexpr (SK) {
+      if (c_lo != 0 || c_hi != nch) {
+        constexpr int kSlab = 64 * Gm::THREADS;  // int32 per slab
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            sk.slab, 0, (int)(G * 2 * kSlab * 4), 0x00020000);
+        const int mine = (int)((g * 2 + (seq == dp_n ? 0 : 1)) * kSlab * 4);
 #pragma unroll
-          for (int bm = 0; bm < 2; ++bm)
+        for (int i4 = 0; i4 < 16; ++i4) {
+          const int bm = i4 >> 3, bn = (i4 >> 2) & 1, r0 = (i4 & 3) * 4;
+          u32x4 v;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rv[bm][q] = rv_pre[bm][q];
-        } else {
-#pragma unroll
-          for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rv[bm][q] = rv_next[bm][q];
+          for (int e = 0; e < 4; ++e)
+            v[e] = (uint32_t)(FLUSH ? acci[bm][bn][r0 + e] : (int)accf[bm][bn][r0 + e]);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rs, (i4 * Gm::THREADS + tid) * 16, mine, 16);
         }
-        if (!okp || (RING_AB == 4 && a.out != (float*)p)) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        const int64_t ut = (tile - sk.q * G) * nch;  // the tile's first unit of the tail
+        // the contributors: the distinct owners of the tile's units (a workgroup whose range
+        // is empty owns none); the ticket counter is the first owner's
+        const int k0 = sk_owner(ut, sk.U, G);
+        int ncon = 0;
+        for (int u = 0, prev = -1; u < nch; ++u) {
+          const int o = sk_owner(ut + u, sk.U, G);
+          ncon += o != prev;
+          prev = o;
+        }
+        uint32_t* flag = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ring_lds) +
+                                                     kZeroOff + 144);
+        if (tid == 0) {
+          const int t = __hip_atomic_fetch_add(sk.cnt + k0, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          const bool last = t == ncon - 1;
+          if (last) __hip_atomic_store(sk.cnt + k0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *flag = last ? 1u : 0u;
+        }
+        __syncthreads();
+        emit = *flag != 0;
+        if (emit) {
+          for (int u = 0, prev = -1; u < nch; ++u) {
+            const int g2 = sk_owner(ut + u, sk.U, G);
+            if (g2 == prev) continue;
+            prev = g2;
+            if (g2 == g) continue;
+            const int64_t first2 = sk.q * G + ((int64_t)g2 * sk.U / G) / nch;
+            const int other = (int)((g2 * 2 + (tile == first2 ? 0 : 1)) * kSlab * 4);
 #pragma unroll
-        for (int bm = 0; bm < 2; ++bm) {
+            for (int i4 = 0; i4 < 16; ++i4) {
+              const int bm = i4 >> 3, bn = (i4 >> 2) & 1, r0 = (i4 & 3) * 4;
+              const u32x4 v = __builtin_bit_cast(
+                  u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (i4 * Gm::THREADS + tid) * 16,
+                                                               other, 16));
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int d = 32 * bm + 8 * q;
-            if (cl + d >= a.Cout) continue;
-            const float4 r = rv[bm][q];
-            const float rr[4] = {r.x, r.y, r.z, r.w};
-            float y[4], o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int acc = FLUSH ? acci[bm][bn][4 * q + e] : (int)accf[bm][bn][4 * q + e];
-              y[e] = fold_acc(acc, (coef_t)cf[2 * (d + e)], (coef_t)cf[2 * (d + e) + 1]) + rr[e];
-              o[e] = y[e] != y[e] ? y[e] : fmaxf(y[e], 0.0f);  // torch.relu keeps NaN
-              y[e] = fmaxf(y[e], 0.0f);                         // TR(NaN) = 0
-            }
-            if (RING_AB == 9) {  // timing only: no stores (values kept live)
-              asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
-              uint32_t qz[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) qz[e] = lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
-              asm volatile("" ::"v"(qz[0]), "v"(qz[1]), "v"(qz[2]), "v"(qz[3]));
-              continue;
-            }
-            if (a.out)
-              *reinterpret_cast<float4*>(a.out + pc + d) = make_float4(o[0], o[1], o[2], o[3]);
-            uint32_t qa[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              qa[e] = RING_AB == 11 ? relu_q(y[e], a.inv_a, a.maxv_a)
-                                    : lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
-            *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d) =
-                make_uint2(qa[0] | (qa[1] << 16), qa[2] | (qa[3] << 16));
-            if (a.codes_b) {
-              uint32_t qb[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) qb[e] = lut_b[relu_q(y[e], a.inv_b, a.maxv_b)];
-              *reinterpret_cast<uint2*>(a.codes_b + p * a.cp_b + cl + d) =
-                  make_uint2(qb[0] | (qb[1] << 16), qb[2] | (qb[3] << 16));
-            }
-            if (cl + d + 4 == a.Cout) {  // the last quad zeroes the pad channels [Cout, cp)
-              if (a.cp_a > a.Cout)
-                *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d + 4) = make_uint2(0, 0);
-              if (a.codes_b && a.cp_b > a.Cout)
-                *reinterpret_cast<uint2*>(a.codes_b + p * a.cp_b + cl + d + 4) = make_uint2(0, 0);
+              for (int e = 0; e < 4; ++e) {
+                if (FLUSH) acci[bm][bn][r0 + e] += (int)v[e];
+                else accf[bm][bn][r0 + e] += (float)(int)v[e];
+              }
             }
           }
         }
-      });
-    } else {
-      static_for<0, 2>([&](auto bmc) __attribute__((always_inline)) {
-        constexpr int bm = decltype(bmc)::value;
-        float4 rv[2][4];
+      }
+    }
+
+    if (emit) {
+      // ---- epilogue from the MFMA layout: lane (r32, hh) of block (bm, bn) holds channels
+      // m0 + wm + 32 bm + 8 q + 4 hh + [0, 4) of pixel column wn + 32 bn + r32
+      if constexpr (FAST) {
+        const int cl = cur.m0 + wm + 4 * hh;  // the lane's first channel
+        const double* cf = coef + 2 * cl;
+        // one pixel block's residual loads at a time (FLUSH: both blocks' would spill)
+        float4 rv_next[2][4];
+        static_for<0, 2>([&](auto bnc) __attribute__((always_inline)) {
+          constexpr int bn = decltype(bnc)::value;
+          const int j = wn + 32 * bn + r32;
+          const int64_t p = cur.p0 + j;
+          const bool okp = j < BNv && p < a.P;
+          const int64_t pc = okp ? p * a.Cout + cl : 0;
+          float4 rv[2][4];
+          if constexpr (FLUSH) {
+            load_res(cur, bn, rv);
+          } else if constexpr (bn == 0) {
+            load_res(cur, 1, rv_next);  // block 1's loads in flight during block 0
 #pragma unroll
-        for (int bn = 0; bn < 2; ++bn)
+            for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int co = cur.m0 + wm + 32 * bm + 8 * q + 4 * hh;
-            const int j = wn + 32 * bn + r32;
-            const int64_t p = cur.p0 + j;
-            const bool ok = a.residual && co < a.Cout && j < BNv && p < a.P;
-            rv[bn][q] = ok ? *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
+              for (int q = 0; q < 4; ++q) rv[bm][q] = rv_pre[bm][q];
+          } else {
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) rv[bm][q] = rv_next[bm][q];
           }
+          if (!okp || (RING_AB == 4 && a.out != (float*)p)) return;
 #pragma unroll
-        for (int bn = 0; bn < 2; ++bn)
+          for (int bm = 0; bm < 2; ++bm) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int co = cur.m0 + wm + 32 * bm + 8 * q + 4 * hh;
-            const int j = wn + 32 * bn + r32;
-            const int64_t p = cur.p0 + j;
-            if (co >= a.Cout || j >= BNv || p >= a.P) continue;
-            if (RING_AB == 4 && a.out != (float*)p) continue;  // timing only: no epilogue
-            int acc4[4];
+            for (int q = 0; q < 4; ++q) {
+              const int d = 32 * bm + 8 * q;
+              if (cl + d >= a.Cout) continue;
+              const float4 r = rv[bm][q];
+              const float rr[4] = {r.x, r.y, r.z, r.w};
+              float y[4], o[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              acc4[e] = FLUSH ? acci[bm][bn][4 * q + e] : (int)accf[bm][bn][4 * q + e];
-            coef_t sc[4], sh[4];
+              for (int e = 0; e < 4; ++e) {
+                const int acc = FLUSH ? acci[bm][bn][4 * q + e] : (int)accf[bm][bn][4 * q + e];
+                y[e] = fold_acc(acc, (coef_t)cf[2 * (d + e)], (coef_t)cf[2 * (d + e) + 1]) + rr[e];
+                o[e] = y[e] != y[e] ? y[e] : fmaxf(y[e], 0.0f);  // torch.relu keeps NaN
+                y[e] = fmaxf(y[e], 0.0f);                         // TR(NaN) = 0
+              }
+              if (RING_AB == 9) {  // timing only: no stores (values kept live)
+                asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+                uint32_t qz[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              sc[e] = (coef_t)coef[2 * (co + e)];
-              sh[e] = (coef_t)coef[2 * (co + e) + 1];
+                for (int e = 0; e < 4; ++e) qz[e] = lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
+                asm volatile("" ::"v"(qz[0]), "v"(qz[1]), "v"(qz[2]), "v"(qz[3]));
+                continue;
+              }
+              if (a.out)
+                *reinterpret_cast<float4*>(a.out + pc + d) = make_float4(o[0], o[1], o[2], o[3]);
+              uint32_t qa[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                qa[e] = RING_AB == 11 ? relu_q(y[e], a.inv_a, a.maxv_a)
+                                      : lut_a[relu_q(y[e], a.inv_a, a.maxv_a)];
+              *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d) =
+                  make_uint2(qa[0] | (qa[1] << 16), qa[2] | (qa[3] << 16));
+              if (a.codes_b) {
+                uint32_t qb[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) qb[e] = lut_b[relu_q(y[e], a.inv_b, a.maxv_b)];
+                *reinterpret_cast<uint2*>(a.codes_b + p * a.cp_b + cl + d) =
+                    make_uint2(qb[0] | (qb[1] << 16), qb[2] | (qb[3] << 16));
+              }
+              if (cl + d + 4 == a.Cout) {  // the last quad zeroes the pad channels [Cout, cp)
+                if (a.cp_a > a.Cout)
+                  *reinterpret_cast<uint2*>(a.codes_a + p * a.cp_a + cl + d + 4) = make_uint2(0, 0);
+                if (a.codes_b && a.cp_b > a.Cout)
+                  *reinterpret_cast<uint2*>(a.codes_b + p * a.cp_b + cl + d + 4) = make_uint2(0, 0);
+              }
             }
-            emit4_nhwc_res(a, p, co, acc4, sc, sh, rv[bn][q], lut_a, lut_b);
           }
-      });
+        });
+      } else {
+        static_for<0, 2>([&](auto bmc) __attribute__((always_inline)) {
+          constexpr int bm = decltype(bmc)::value;
+          float4 rv[2][4];
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int co = cur.m0 + wm + 32 * bm + 8 * q + 4 * hh;
+              const int j = wn + 32 * bn + r32;
+              const int64_t p = cur.p0 + j;
+              const bool ok = a.residual && co < a.Cout && j < BNv && p < a.P;
+              rv[bn][q] = ok ? *reinterpret_cast<const float4*>(a.residual + p * a.Cout + co)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int co = cur.m0 + wm + 32 * bm + 8 * q + 4 * hh;
+              const int j = wn + 32 * bn + r32;
+              const int64_t p = cur.p0 + j;
+              if (co >= a.Cout || j >= BNv || p >= a.P) continue;
+              if (RING_AB == 4 && a.out != (float*)p) continue;  // timing only: no epilogue
+              int acc4[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc4[e] = FLUSH ? acci[bm][bn][4 * q + e] : (int)accf[bm][bn][4 * q + e];
+              coef_t sc[4], sh[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                sc[e] = (coef_t)coef[2 * (co + e)];
+                sh[e] = (coef_t)coef[2 * (co + e) + 1];
+              }
+              emit4_nhwc_res(a, p, co, acc4, sc, sh, rv[bn][q], lut_a, lut_b);
+            }
+        });
+      }
     }
 
     if (!has_next) break;
     // ---- next tile: its patch chunk 0 and weight steps 0/1 are already staged or in flight
-    tile = ntile;
+    ++seq;
+    tile = tile_at(seq);
     cur = nxt;
-    ntile = tile + G;
-    nxt = ring_tile(a, ntile < T ? ntile : tile, R, mt, a.m_slow, ptc);
+    nxt = ring_tile(a, tile_at(seq + 1 < n_seq ? seq + 1 : seq), R, mt, a.m_slow, ptc);
+    c_lo = chunk_lo(seq);
+    c_hi = chunk_hi(seq);
     setup_b(cur);
     // its first fragments (the last step of the previous tile prefetched this tile's
     // weights but the old pixels): step 0's image and patch were retired by the barrier of
@@ -593,19 +715,19 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
   }
 }
 
-template <int NW, int KS, int PI, bool FLUSH, bool FAST>
+template <int NW, int KS, int PI, bool FLUSH, bool FAST, bool SK>
 hipError_t launch_ring_fast(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
-                            hipStream_t stream) {
+                            const RingSk& sk, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv2d_tp_ring_kernel<NW, KS, PI, FLUSH, FAST>),
+        reinterpret_cast<const void*>(&conv2d_tp_ring_kernel<NW, KS, PI, FLUSH, FAST, SK>),
         hipFuncAttributeMaxDynamicSharedMemorySize, RingGeom<NW, KS>::BUDGET);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  conv2d_tp_ring_kernel<NW, KS, PI, FLUSH, FAST>
-      <<<dim3((unsigned)grid), 64 * NW, lds, stream>>>(a, R, ptc);
+  conv2d_tp_ring_kernel<NW, KS, PI, FLUSH, FAST, SK>
+      <<<dim3((unsigned)grid), 64 * NW, lds, stream>>>(a, R, ptc, sk);
   return hipGetLastError();
 }
 
@@ -615,16 +737,85 @@ bool ring_fast_epilogue(const ConvArgs& a) {
          (a.codes_b == nullptr || (a.lut_b > 0 && a.fmt_b == kCodesF16));
 }
 
-template <int NW, int KS, int PI>
-hipError_t launch_ring_pi(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
-                          hipStream_t stream) {
+template <int NW, int KS, int PI, bool SK>
+hipError_t launch_ring_sk(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
+                          const RingSk& sk, hipStream_t stream) {
   const bool flush = a.kc_steps != 0;  // 0: the whole K range is one exact window
   const bool fast = ring_fast_epilogue(a);
   if (flush)
-    return fast ? launch_ring_fast<NW, KS, PI, true, true>(a, R, ptc, grid, lds, stream)
-                : launch_ring_fast<NW, KS, PI, true, false>(a, R, ptc, grid, lds, stream);
-  return fast ? launch_ring_fast<NW, KS, PI, false, true>(a, R, ptc, grid, lds, stream)
-              : launch_ring_fast<NW, KS, PI, false, false>(a, R, ptc, grid, lds, stream);
+    return fast ? launch_ring_fast<NW, KS, PI, true, true, SK>(a, R, ptc, grid, lds, sk, stream)
+                : launch_ring_fast<NW, KS, PI, true, false, SK>(a, R, ptc, grid, lds, sk, stream);
+  return fast ? launch_ring_fast<NW, KS, PI, false, true, SK>(a, R, ptc, grid, lds, sk, stream)
+              : launch_ring_fast<NW, KS, PI, false, false, SK>(a, R, ptc, grid, lds, sk, stream);
+}
+
+// sk == nullptr: the data-parallel tile stream; else the stream-K split (8-wave shape only)
+template <int NW, int KS, int PI>
+hipError_t launch_ring_pi(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
+                          const RingSk* sk, hipStream_t stream) {
+  if constexpr (NW == 8)
+    if (sk) return launch_ring_sk<NW, KS, PI, true>(a, R, ptc, grid, lds, *sk, stream);
+  return launch_ring_sk<NW, KS, PI, false>(a, R, ptc, grid, lds, RingSk{}, stream);
+}
+
+// ---- stream-K workspaces, one per (device, stream): a kernel on another stream may run
+// concurrently, so no two streams share slabs or counters.  Allocated (and the counters
+// zeroed) at the first split launch on a stream; a stream being captured into a graph that
+// has none runs the data-parallel stream instead (same results).
+struct SkWorkspace {
+  int dev;
+  hipStream_t stream;
+  int* base;  // [1024] counters | slabs
+  int64_t slab_ints;
+};
+constexpr int kSkMaxGrid = 1024;
+constexpr int kSkMaxWorkspaces = 16;
+std::mutex g_sk_mu;
+SkWorkspace g_sk_ws[kSkMaxWorkspaces];
+int g_sk_n = 0;
+
+bool sk_workspace(hipStream_t stream, int64_t grid, int64_t slab_ints, RingSk* sk) {
+  if (grid > kSkMaxGrid) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  SkWorkspace* w = nullptr;
+  for (int i = 0; i < g_sk_n; ++i)
+    if (g_sk_ws[i].dev == dev && g_sk_ws[i].stream == stream) w = &g_sk_ws[i];
+  if (w && w->slab_ints < grid * slab_ints) return false;  // (grid is fixed per device)
+  if (!w) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
+      return false;
+    if (g_sk_n == kSkMaxWorkspaces) return false;
+    // room for the device's default grid, so later launches never outgrow it
+    const int64_t ints = (grid > device_cus() ? grid : device_cus()) * slab_ints;
+    int* base = nullptr;
+    if (hipMalloc(&base, (size_t)(kSkMaxGrid + ints) * sizeof(int)) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (hipMemsetAsync(base, 0, kSkMaxGrid * sizeof(int), stream) != hipSuccess) {
+      (void)hipFree(base);
+      return false;
+    }
+    w = &g_sk_ws[g_sk_n++];
+    *w = SkWorkspace{dev, stream, base, ints};
+  }
+  sk->cnt = w->base;
+  sk->slab = w->base + kSkMaxGrid;
+  return true;
+}
+
+// TQ_RING_SK: 0 (default) = data-parallel tiles only; 1 = a stream-K tail when it shortens the
+// longest per-workgroup chunk list with at most one tail chunk per workgroup; 3 = whenever it
+// shortens that list; 2 = a tail of about half the tiles whenever tiles are left over (tests).
+// Measured (profiles/r04_ring_streamk_ab.txt): mode 1 equal-to-slower on layer 2, mode 3
+// 40-45 % slower on layers 3/4 -- the SK instantiations spill more in the K loop, and an
+// all-CU MFMA loop runs each step slower (the round-3 patch-engine finding)
+int ring_sk_mode() {
+  const char* v = getenv("TQ_RING_SK");
+  return v ? atoi(v) : 0;
 }
 
 // Largest patch (pixels) over every tile: the row pattern repeats every Ho / gcd(R, Ho) tiles.
@@ -676,14 +867,35 @@ hipError_t launch_ring_shape(const ConvArgs& a, const RingPlan& pl, int per_cu,
   int64_t grid = (int64_t)per_cu * device_cus();
   const char* genv = getenv("TQ_RING_GRID");  // tests: fewer workgroups, more tiles each
   if (genv && atoi(genv) > 0) grid = atoi(genv);
-  if (grid > tiles) grid = tiles;
+  // stream-K tail (8-wave shape, RingSk; opt-in, ring_sk_mode): after q full rounds the r
+  // tiles left are split into their r * nch chunks over the whole grid, so the longest list
+  // is q nch + ceil(r nch / G) chunks instead of (q + 1) nch
+  RingSk sk{};
+  const RingSk* skp = nullptr;
+  const int skm = ring_sk_mode();
+  if (NW == 8 && skm > 0) {
+    const int64_t nch = a.Cp / KS;
+    int64_t q = tiles / grid;
+    if (skm == 2) q /= 2;  // tests: a longer tail, ranges over several tiles
+    const int64_t r = tiles - q * grid;
+    const int64_t U = r * nch;
+    const int64_t dp_max = (tiles + grid - 1) / grid * nch;
+    const int64_t sk_max = q * nch + (U + grid - 1) / grid;
+    const bool want = skm == 2 ? r > 0 : r > 0 && sk_max < dp_max && (skm == 3 || U <= grid);
+    if (nch > 1 && want && sk_workspace(stream, grid, 2 * 64 * RingGeom<NW, KS>::THREADS, &sk)) {
+      sk.U = U;
+      sk.q = q;
+      skp = &sk;
+    }
+  }
+  if (!skp && grid > tiles) grid = tiles;
   const size_t lds = (size_t)pl.lds;
   hipError_t e = hipErrorInvalidValue;
   static_for<3, 7>([&](auto pc) {
     constexpr int PI = decltype(pc)::value;
     constexpr int NR = RingGeom<NW, KS>::slots(PI);
     if constexpr (NR >= 3 && PI <= 10 - NR)  // the shapes ring_plan can choose
-      if (pl.pi == PI) e = launch_ring_pi<NW, KS, PI>(a, pl.R, ptc, grid, lds, stream);
+      if (pl.pi == PI) e = launch_ring_pi<NW, KS, PI>(a, pl.R, ptc, grid, lds, skp, stream);
   });
   return e;
 }

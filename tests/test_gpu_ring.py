@@ -124,3 +124,36 @@ def test_ring_m_slow_order(monkeypatch):
     got = _run(cm, lay_m, 512, 7, cfg=RING, sc=sc, sh=sh, res=res, kc_steps=lay_m.kc_steps,
                kc_chunk=lay_m.kc_chunk)
     assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("cin,cout,hw,batch", [
+    (128, 128, 28, 5),    # 2 chunks per tile
+    (256, 256, 14, 6),    # 4 chunks, two Cout tiles
+    (512, 512, 7, 9),     # 8 chunks, four Cout tiles: with 37 workgroups a tile spans up to 6
+    (192, 132, 9, 3),     # 3 chunks, partial Cout tile
+])
+@pytest.mark.parametrize("grid", ["0", "3", "7", "37"])
+def test_ring_stream_k_bit_identical(cin, cout, hw, batch, grid, shape, monkeypatch):
+    """Stream-K split (TQ_RING_SK=2 forces it wherever it applies): tiles split at chunk
+    boundaries over 2..6 workgroups, the last contributor adding the others' int32 slabs --
+    the same bits as the VALU engine, with and without int32 exactness windows; every launch
+    leaves its tile counters at zero for the next one (the cases share one workspace)."""
+    conv, x, sc, sh, res = _case(cin, cout, hw, batch, seed=cin + 7 * cout + hw)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, cout, hw, cfg=0, sc=sc, sh=sh, res=res, codes_b=True,
+               fmt=torch.int16)
+    monkeypatch.setenv("TQ_RING_GRID", grid)
+    monkeypatch.setenv("TQ_RING_SK", "2")
+    for kc in ((lay_m.kc_steps, lay_m.kc_chunk), (lay_m.kc_steps_nonneg, lay_m.kc_chunk_nonneg),
+               (1, 1)):
+        for form in ("res", "codes_only"):
+            if form == "res":
+                r = ref
+                got = _run(cm, lay_m, cout, hw, cfg=RING, sc=sc, sh=sh, res=res, codes_b=True,
+                           kc_steps=kc[0], kc_chunk=kc[1])
+            else:
+                r = _run(cv, lay_v, cout, hw, cfg=0, sc=sc, sh=sh, out=False, fmt=torch.int16)
+                got = _run(cm, lay_m, cout, hw, cfg=RING, sc=sc, sh=sh, out=False,
+                           kc_steps=kc[0], kc_chunk=kc[1])
+            for g, e in zip(got, r):
+                assert (g is None and e is None) or torch.equal(g, e), (kc, form)
