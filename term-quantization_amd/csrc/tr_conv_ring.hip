@@ -171,10 +171,11 @@ __device__ __forceinline__ half8 lds_frag(uint32_t byte_addr) {
                  (uintptr_t)byte_addr));
 }
 
-// FAST: the fused ResNet executor's epilogue form, specialised at launch -- ReLU, fp16 codes
-// from the code tables (every code output has one), Cout % 4 == 0 -- with per-pixel base
-// pointers and compile-time channel offsets; other forms run the shared emit4_nhwc_res.
-template <int NW, int KS, int PI, bool FLUSH, bool FAST, bool SK>
+// FAST: the fused ResNet executor's epilogue forms, specialised at launch (ring_epilogue_form)
+// -- 1: ReLU, fp16 codes from the code tables (every code output has one); 2: ReLU and the
+// fp32 output only (the last conv) -- Cout % 4 == 0, with per-pixel base pointers and
+// compile-time channel offsets; other forms (0) run the shared emit4_nhwc_res.
+template <int NW, int KS, int PI, bool FLUSH, int FAST, bool SK>
 __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, int R,
                                                                    int64_t ptc, RingSk sk) {
   using Gm = RingGeom<NW, KS>;
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
         else
           issue_w(nm0, t + NR - 1 - kRingTaps, nc, 0, nlive, slot_off(t + NR - 1));
         if constexpr (t < PI) issue_piece(t, nsrc0, npx, buf ^ 1);
-        if constexpr (FAST && !FLUSH && t == kRingTaps - 1) {
+        if constexpr (FAST != 0 && !FLUSH && t == kRingTaps - 1) {
           if (last_chunk) load_res(cur, 0, rv_pre);
         }
         // (3) B addresses of step s+1 (next tap, or tap 0 of the next chunk's buffer)
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
     if (emit) {
       // ---- epilogue from the MFMA layout: lane (r32, hh) of block (bm, bn) holds channels
       // m0 + wm + 32 bm + 8 q + 4 hh + [0, 4) of pixel column wn + 32 bn + r32
-      if constexpr (FAST) {
+      if constexpr (FAST != 0) {
         const int cl = cur.m0 + wm + 4 * hh;  // the lane's first channel
         const double* cf = coef + 2 * cl;
         // one pixel block's residual loads at a time (FLUSH: both blocks' would spill)
@@ -630,8 +631,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
                 asm volatile("" ::"v"(qz[0]), "v"(qz[1]), "v"(qz[2]), "v"(qz[3]));
                 continue;
               }
-              if (a.out)
+              if (FAST == 2 || a.out)
                 *reinterpret_cast<float4*>(a.out + pc + d) = make_float4(o[0], o[1], o[2], o[3]);
+              if constexpr (FAST == 2) continue;  // (form 2: no code outputs)
               uint32_t qa[4];
 #pragma unroll
               for (int e = 0; e < 4; ++e)
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
   }
 }
 
-template <int NW, int KS, int PI, bool FLUSH, bool FAST, bool SK>
+template <int NW, int KS, int PI, bool FLUSH, int FAST, bool SK>
 hipError_t launch_ring_fast(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
                             const RingSk& sk, hipStream_t stream) {
   static bool attr_set = false;
@@ -731,22 +733,31 @@ hipError_t launch_ring_fast(const ConvArgs& a, int R, int64_t ptc, int64_t grid,
   return hipGetLastError();
 }
 
-// the FAST epilogue's form: ReLU, fp16 codes_a (+ codes_b) each served by a code table
-bool ring_fast_epilogue(const ConvArgs& a) {
+// the specialised epilogue form (the kernel's FAST): 1 = ReLU + fp16 codes_a (+ codes_b) each
+// served by a code table; 2 = ReLU + fp32 output, no codes (TQ_EPI_FAST=0: generic only); 0
+bool ring_codes_form(const ConvArgs& a) {
   return a.relu == 1 && a.codes_a != nullptr && a.lut_a > 0 && a.fmt_a == kCodesF16 &&
          (a.codes_b == nullptr || (a.lut_b > 0 && a.fmt_b == kCodesF16));
+}
+int ring_epilogue_form(const ConvArgs& a) {
+  if (ring_codes_form(a)) return 1;
+  const char* v = getenv("TQ_EPI_FAST");
+  if (v && atoi(v) == 0) return 0;
+  return a.relu == 1 && a.out != nullptr && a.codes_a == nullptr && a.codes_b == nullptr ? 2 : 0;
 }
 
 template <int NW, int KS, int PI, bool SK>
 hipError_t launch_ring_sk(const ConvArgs& a, int R, int64_t ptc, int64_t grid, size_t lds,
                           const RingSk& sk, hipStream_t stream) {
   const bool flush = a.kc_steps != 0;  // 0: the whole K range is one exact window
-  const bool fast = ring_fast_epilogue(a);
-  if (flush)
-    return fast ? launch_ring_fast<NW, KS, PI, true, true, SK>(a, R, ptc, grid, lds, sk, stream)
-                : launch_ring_fast<NW, KS, PI, true, false, SK>(a, R, ptc, grid, lds, sk, stream);
-  return fast ? launch_ring_fast<NW, KS, PI, false, true, SK>(a, R, ptc, grid, lds, sk, stream)
-              : launch_ring_fast<NW, KS, PI, false, false, SK>(a, R, ptc, grid, lds, sk, stream);
+  hipError_t e = hipErrorInvalidValue;
+  static_for<0, 3>([&](auto fc) {
+    constexpr int F = decltype(fc)::value;
+    if (F != ring_epilogue_form(a)) return;
+    e = flush ? launch_ring_fast<NW, KS, PI, true, F, SK>(a, R, ptc, grid, lds, sk, stream)
+              : launch_ring_fast<NW, KS, PI, false, F, SK>(a, R, ptc, grid, lds, sk, stream);
+  });
+  return e;
 }
 
 // sk == nullptr: the data-parallel tile stream; else the stream-K split (8-wave shape only)

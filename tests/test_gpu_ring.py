@@ -29,21 +29,24 @@ def shape(request, monkeypatch):
 
 
 def _run(codes, lay, cout, hw, *, cfg, sc, sh, res=None, relu=True, out=True, codes_b=False,
-         fmt=torch.float16, kc_steps=0, kc_chunk=-1):
+         fmt=torch.float16, kc_steps=0, kc_chunk=-1, codes_a=True):
     n = codes.shape[0]
     o = torch.full((n, cout, hw, hw), float("nan"), device=DEV).contiguous(
         memory_format=torch.channels_last) if out else None
     cpo = tq_ops.act_channels(cout)
-    ca = torch.full((n, hw, hw, cpo), 7, dtype=torch.int16, device=DEV).to(fmt)
+    ca = torch.full((n, hw, hw, cpo), 7, dtype=torch.int16, device=DEV).to(fmt) \
+        if codes_a else None
     cb = torch.full((n, hw, hw, cpo), 7, dtype=torch.int16, device=DEV).to(fmt) \
         if codes_b else None
     tq_native.conv2d_termpair_fused(codes, lay.w_codes, cout, 3, 3, (1, 1), (1, 1), (1, 1),
                                     hw, hw, out=o, ch_scale=sc, ch_shift=sh, residual=res,
-                                    relu=relu, codes_a=ca, quant_a=(0.05, 9, 3), codes_b=cb,
+                                    relu=relu, codes_a=ca,
+                                    quant_a=(0.05, 9, 3) if codes_a else None, codes_b=cb,
                                     quant_b=(0.11, 9, 2) if codes_b else None, config=cfg,
                                     kc_steps=kc_steps, kc_chunk=kc_chunk)
     torch.cuda.synchronize()
-    return (None if o is None else o.view(torch.int32).cpu(), ca.float().cpu(),
+    return (None if o is None else o.view(torch.int32).cpu(),
+            None if ca is None else ca.float().cpu(),
             None if cb is None else cb.float().cpu())
 
 
@@ -98,14 +101,20 @@ def test_ring_bit_identical_to_valu(cin, cout, hw, batch, grid, monkeypatch):
         assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]), kc
 
 
-@pytest.mark.parametrize("form", ["codes_only", "no_relu", "out_only"])
+@pytest.mark.parametrize("form", ["codes_only", "no_relu", "out_only", "last_conv",
+                                  "last_conv_generic"])
 def test_ring_epilogue_forms(form, monkeypatch):
     """The fused executor's other epilogue forms: codes only (no fp32 output, no residual),
-    signed values (no ReLU: code tables negated), fp32 output without codes_b."""
+    signed values (no ReLU: code tables negated), fp32 output without codes_b, and the last
+    conv's ReLU + residual + fp32 output with no codes (specialised form 2; TQ_EPI_FAST=0
+    the generic epilogue)."""
     conv, x, sc, sh, res = _case(256, 256, 14, 4, seed=3)
     lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
     kw = dict(codes_only=dict(out=False), no_relu=dict(relu=False, res=res),
-              out_only=dict(res=res))[form]
+              out_only=dict(res=res), last_conv=dict(res=res, codes_a=False),
+              last_conv_generic=dict(res=res, codes_a=False))[form]
+    if form == "last_conv_generic":
+        monkeypatch.setenv("TQ_EPI_FAST", "0")
     ref = _run(cv, lay_v, 256, 14, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
     monkeypatch.setenv("TQ_RING_GRID", "5")
     got = _run(cm, lay_m, 256, 14, cfg=RING, sc=sc, sh=sh, kc_steps=lay_m.kc_steps,
