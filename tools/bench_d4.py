@@ -91,6 +91,13 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
+def timed_median(fn, steps, warmup, reps=3):
+    """Median over `reps` back-to-back timed loops of `steps` steps (one host hiccup in an
+    eager launch loop of ~100 launches per step otherwise moves a short loop's mean)."""
+    ts = [timed(fn, steps, warmup if i == 0 else 0) for i in range(reps)]
+    return sorted(ts)[len(ts) // 2]
+
+
 def timed_graph(fn, steps, warmup):
     """fn captured once as a hipGraph and replayed (no per-kernel host launches); None when
     the capture fails."""
@@ -218,10 +225,10 @@ def cnn_fused(arch, steps, warmup, batch, dev, nstreams=2):
         tr_layer.set_tr_tracking(q, False)
         ex = (tq_fuse.FusedMobileNetV2 if arch == "mobilenet_v2" else
               tq_fuse.FusedEfficientNet)(q)
-        tf1 = timed(lambda: ex(x), steps, warmup)
+        tf1 = timed_median(lambda: ex(x), steps, warmup)
         streams = [torch.cuda.Stream() for _ in range(nstreams)]
         # image chunks on their own streams (tq_fuse forward_streams): the measured rate
-        tf = timed(lambda: ex.forward_streams(x, streams), steps, warmup)
+        tf = timed_median(lambda: ex.forward_streams(x, streams), steps, warmup)
         # per-kernel rooflines from one-stream launches (concurrent launches share the GPU)
         kern = kernel_breakdown(lambda: ex(x), steps, tf1)
     tp = kern.get("conv2d_termpair")
@@ -230,10 +237,11 @@ def cnn_fused(arch, steps, warmup, batch, dev, nstreams=2):
     dom = max(kern, key=lambda k: kern[k]["share_of_step"])
     return {"images_per_s": batch / tf, "ms_per_step": tf * 1e3, "batch": batch,
             "streams": nstreams, "images_per_s_one_stream": batch / tf1,
+            "timing": "median of 3 loops of %d eager steps each" % steps,
             "dominant_kernel": dom, "kernels": kern}
 
 
-def d4_summary(dev, steps=5, warmup=2, batch=256):
+def d4_summary(dev, steps=10, warmup=3, batch=256):
     """BASELINE configs[2] and [3] on one GPU, compactly (bench.py's "d4" key): LSTM-650
     tokens/s (term-pair layer-0 path and the MIOpen composition) with the term-pair decoder
     GEMM's roofline; fused MobileNet-V2 / EfficientNet-b0 images/s with per-kernel rooflines."""
