@@ -47,6 +47,9 @@
 #ifndef RING_AB
 #define RING_AB 0  // timing-only ablation builds (tools/variant.sh); 0 = the product kernel
 #endif
+#ifndef RING_DMA_LATE
+#define RING_DMA_LATE 0  // 1: a step's DMA issued after its first substep (A/B builds)
+#endif
 
 namespace tq {
 
@@ -429,12 +432,16 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
         if constexpr (RING_AB != 5) __builtin_amdgcn_s_barrier();  // (5: timing only)
         asm volatile("" ::: "memory");
         // (2) weight image of step s+NR-1 into the slot of step s-1; one patch piece of the
-        // next chunk
-        if constexpr (t + NR - 1 < kRingTaps)
-          issue_w(cur.m0, t + NR - 1, c, 0, true, slot_off(t + NR - 1));
-        else
-          issue_w(nm0, t + NR - 1 - kRingTaps, nc, 0, nlive, slot_off(t + NR - 1));
-        if constexpr (t < PI) issue_piece(t, nsrc0, npx, buf ^ 1);
+        // next chunk (RING_DMA_LATE: after substep 0's MFMAs, so the matrix cores restart
+        // before the ~60-185 cycles per DMA issue)
+        auto issue_dma = [&]() __attribute__((always_inline)) {
+          if constexpr (t + NR - 1 < kRingTaps)
+            issue_w(cur.m0, t + NR - 1, c, 0, true, slot_off(t + NR - 1));
+          else
+            issue_w(nm0, t + NR - 1 - kRingTaps, nc, 0, nlive, slot_off(t + NR - 1));
+          if constexpr (t < PI) issue_piece(t, nsrc0, npx, buf ^ 1);
+        };
+        if constexpr (!RING_DMA_LATE) issue_dma();
         if constexpr (FAST != 0 && !FLUSH && t == kRingTaps - 1) {
           if (last_chunk) load_res(cur, 0, rv_pre);
         }
@@ -476,6 +483,8 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
           // MFMAs (the scheduler otherwise recycles one fragment register: read, wait, MFMA)
           __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS reads
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMAs
+          if constexpr (RING_DMA_LATE != 0)
+            if (k == 0) issue_dma();
         }
         // after SUB (even) substeps the next step's fragments sit in buffer 0 again
         bcur[0] = bnx[0];
