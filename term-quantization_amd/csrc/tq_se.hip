@@ -22,7 +22,9 @@ namespace tq {
 
 namespace {
 
-constexpr int kSeThreads = 256;
+// 16 waves: the launch has only N workgroups (one per image, fewer than the CUs), so one
+// workgroup's latency is the kernel's time -- spread each image's outputs over more waves
+constexpr int kSeThreads = 1024;
 constexpr int kSeU = 8;  // weight loads in flight per lane
 
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
