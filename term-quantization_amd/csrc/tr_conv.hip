@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
     const float* __restrict__ ch_shift, const float* __restrict__ gate, int act,
     float* __restrict__ out,
     int16_t* __restrict__ codes, int64_t npix, int64_t HW, int C, int Cp, double inv_sf,
-    float maxv, int k, int fmt, int lut_n) {
+    float maxv, int k, int fmt, int lut_n, int fixed_chunk) {
   // the code table (lut_n = maxv + 1 entries, 0 = none): TR of a value costs its a1
   // rounding and one LDS read (tq_device.h lut_codes; signed values after swish / a gate too)
   extern __shared__ __attribute__((aligned(16))) uint16_t lut[];
@@ -441,10 +441,28 @@ __global__ __launch_bounds__(256) void act_encode_act_kernel(
   const IDX chunks = (IDX)(Cp / 8);
   const IDX total = (IDX)npix * chunks;
   const IDX hw = (IDX)HW;
-  for (IDX t = (IDX)blockIdx.x * 256 + threadIdx.x; t < total; t += (IDX)gridDim.x * 256) {
-    const IDX pix = t / chunks;
-    const int c0 = (int)(t - pix * chunks) * 8;
-    const IDX img = pix / hw;
+  const double inv_hw = 1.0 / (double)HW;
+  // fixed_chunk: the grid stride is a multiple of the chunks per pixel, so a lane keeps its
+  // channel chunk and steps whole pixels -- no integer division per iteration; the image
+  // index comes from a double reciprocal (exact after the one correction: pix < 2^32)
+  const IDX t0 = (IDX)blockIdx.x * 256 + threadIdx.x;
+  const IDX stride = (IDX)gridDim.x * 256;
+  const IDX pstep = fixed_chunk ? stride / chunks : 0;
+  IDX fpix = fixed_chunk ? t0 / chunks : 0;
+  const int fc0 = fixed_chunk ? (int)(t0 - fpix * chunks) * 8 : 0;
+  for (IDX t = t0; t < total; t += stride, fpix += pstep) {
+    IDX pix, img;
+    int c0;
+    if (fixed_chunk) {
+      pix = fpix;
+      c0 = fc0;
+      img = (IDX)((double)pix * inv_hw);
+      if (pix - img * hw >= hw) ++img;
+    } else {
+      pix = t / chunks;
+      c0 = (int)(t - pix * chunks) * 8;
+      img = pix / hw;
+    }
     float v[8];
     const bool vec = c0 + 8 <= C && (C & 3) == 0;
     if (vec) {
@@ -538,16 +556,29 @@ hipError_t launch_act_encode_act(const float* x, const float* ch_scale, const fl
   const char* lut_env = getenv("TQ_LUT");  // 0: computed codes (tests, A/B; read per launch)
   const int lut_n = (!(lut_env && atoi(lut_env) == 0) && inv > 0.0 && inv <= 1.0e308 &&
                      (int)maxv + 1 <= kLutMax) ? (int)maxv + 1 : 0;
-  const int64_t grid = std::min<int64_t>((n + 255) / 256, (int64_t)device_cus() * 8);
+  int64_t grid = std::min<int64_t>((n + 255) / 256, (int64_t)device_cus() * 8);
+  // a grid whose stride (grid * 256 lanes) is a multiple of the chunks per pixel: every lane
+  // keeps one channel chunk (TQ_AEA_FIXED=0: the per-iteration division form, A/B)
+  const int64_t chunks = Cp / 8;
+  int64_t g = 256, r = chunks;
+  while (r) {
+    const int64_t t = g % r;
+    g = r;
+    r = t;
+  }
+  const int64_t m = chunks / g;  // grid granule
+  const char* fenv = getenv("TQ_AEA_FIXED");
+  int fixed = !(fenv && atoi(fenv) == 0) && grid >= m;
+  if (fixed) grid = grid / m * m;
   const bool small = n < (1ll << 31) && npix * Cp < (1ll << 31);
   if (small)
     act_encode_act_kernel<uint32_t><<<dim3((unsigned)grid), 256, (size_t)lut_n * 2, stream>>>(
         x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, inv, maxv,
-        k, fmt, lut_n);
+        k, fmt, lut_n, fixed);
   else
     act_encode_act_kernel<int64_t><<<dim3((unsigned)grid), 256, (size_t)lut_n * 2, stream>>>(
         x, ch_scale, ch_shift, gate, act, out, codes, npix, H * W, (int)C, (int)Cp, inv, maxv,
-        k, fmt, lut_n);
+        k, fmt, lut_n, fixed);
   return hipGetLastError();
 }
 

@@ -429,6 +429,26 @@ def test_act_encode_act_code_table_bit_identical(act, gated, fmt, monkeypatch):
     assert (res[0][0][..., c:] == 0).all()
 
 
+@pytest.mark.parametrize("c,cp", [(200, 200), (44, 48)])
+def test_act_encode_act_fixed_chunk_grid(c, cp, monkeypatch):
+    """A grid-stride wide enough that lanes walk several pixels across image boundaries: the
+    fixed-chunk loop (grid stride a multiple of the chunks per pixel, image index from a
+    reciprocal) gives the per-iteration-division loop's bits (TQ_AEA_FIXED=0)."""
+    n, hw = 4, 112
+    torch.manual_seed(11)
+    x = torch.randn(n, c, hw, hw, device=DEV).contiguous(memory_format=torch.channels_last)
+    gate = torch.rand(n, c, device=DEV)
+    res = []
+    for fixed in ("1", "0"):
+        monkeypatch.setenv("TQ_AEA_FIXED", fixed)
+        codes = torch.full((n, hw, hw, cp), 77, dtype=torch.float16, device=DEV)
+        out = torch.empty_like(x)
+        tq_native.act_encode_act(x, 0.05, 9, 3, codes, act="swish", gate=gate, out=out)
+        res.append((codes.float().cpu(), out.view(torch.int32).cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert (res[0][0] != 77).all()
+
+
 def test_fused_resnet_specialised_epilogues_bit_identical(monkeypatch):
     """The engines' epilogues specialised to the executor's ReLU + code-table form (direct
     engine emit4_relu_lut, TQ_EPI_FAST) give the generic epilogue's bits: every captured conv
