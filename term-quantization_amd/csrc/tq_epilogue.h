@@ -148,15 +148,42 @@ __device__ __forceinline__ void emit4_identity(const ConvArgs& a, int64_t p, int
                   fold_acc(acc[2], sc[2], sh[2]), fold_acc(acc[3], sc[3], sh[3]));
 }
 
+// The linear form (no activation: a depthwise net's projection conv, optional residual and
+// fp32 output, one code output from its table -- signed values, tq_device.h lut_codes) of
+// emit4_nhwc_res.
+__device__ __forceinline__ void emit4_linear_lut(const ConvArgs& a, int64_t p, int co,
+                                                 const int acc[4], const coef_t sc[4],
+                                                 const coef_t sh[4], const float4 rv,
+                                                 const uint16_t* lut_a) {
+  const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    y[i] = fold_acc(acc[i], sc[i], sh[i]);
+    if (a.residual) y[i] += r[i];
+  }
+  if (a.out)
+    *reinterpret_cast<float4*>(a.out + p * a.Cout + co) = make_float4(y[0], y[1], y[2], y[3]);
+  uint32_t v[4];
+  lut_codes<4>(y, a.inv_a, a.maxv_a, a.fmt_a, false, lut_a, v);
+  *reinterpret_cast<int2*>(a.codes_a + p * a.cp_a + co) =
+      make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+  if (co + 4 == a.Cout && a.cp_a > a.Cout)
+    *reinterpret_cast<int2*>(a.codes_a + p * a.cp_a + co + 4) = make_int2(0, 0);
+}
+
 // Epilogue form of a conv launch the engines specialise (0 = the generic emit4_nhwc(_res)):
 // 1 = ReLU with every code output from its table (emit4_relu_lut), 2 = the identity form
-// (emit4_identity).  TQ_EPI_FAST=0 keeps the generic epilogue (tests, A/B).
+// (emit4_identity), 3 = the linear form with one table-served code output (emit4_linear_lut;
+// the direct engine only -- the others run 0 for it).  TQ_EPI_FAST=0 keeps the generic
+// epilogue (tests, A/B).
 __host__ inline int epilogue_form(const ConvArgs& a) {
   const char* env = getenv("TQ_EPI_FAST");
   if ((env && atoi(env) == 0) || (a.Cout & 3) || a.ds_x) return 0;
   if (a.relu == 1 && a.codes_a && a.lut_a > 0 && (a.codes_b == nullptr || a.lut_b > 0))
     return 1;
   if (a.relu == 0 && a.out && !a.codes_a && !a.codes_b && !a.residual) return 2;
+  if (a.relu == 0 && a.codes_a && a.lut_a > 0 && !a.codes_b) return 3;
   return 0;
 }
 

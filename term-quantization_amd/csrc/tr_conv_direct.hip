@@ -77,7 +77,8 @@ struct DirCfg {
 // main conv's, into fresh fp32 accumulators, while the main conv's sums wait in int32; the
 // epilogue turns them into the identity (what the separate downsample conv would store) and
 // adds it where a residual read from HBM would go.
-// EPI: tq_epilogue.h epilogue_form (1 ReLU + code tables, 2 identity; the host picks it)
+// EPI: tq_epilogue.h epilogue_form (1 ReLU + code tables, 2 identity, 3 linear + one code
+// table; the host picks it)
 template <int MB, bool FLUSH, bool DS, bool SWISH, int EPI = 0>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
@@ -427,6 +428,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
         emit4_relu_lut(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
       else if constexpr (EPI == 2)
         emit4_identity(a, p, c4, acc4, psc, psh);
+      else if constexpr (EPI == 3)
+        emit4_linear_lut(a, p, c4, acc4, psc, psh, rv, lut_a);
       else
         emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
     }
@@ -461,6 +464,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
       emit4_relu_lut(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);  // (host: vec)
     else if constexpr (EPI == 2)
       emit4_identity(a, p, co, acc4, sc, sh);
+    else if constexpr (EPI == 3)
+      emit4_linear_lut(a, p, co, acc4, sc, sh, res[it], lut_a);  // (host: vec)
     else if (vec)
       emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
@@ -698,6 +703,9 @@ hipError_t launch_direct_mb(const ConvArgs& a, hipStream_t stream) {
   if (form == 2)
     return flush ? launch_direct_cfg<1, true, false, false, 2>(a, stream)
                  : launch_direct_cfg<1, false, false, false, 2>(a, stream);
+  if (form == 3)
+    return flush ? launch_direct_cfg<1, true, false, false, 3>(a, stream)
+                 : launch_direct_cfg<1, false, false, false, 3>(a, stream);
   return flush ? launch_direct_cfg<MB, true, DS>(a, stream)
                : launch_direct_cfg<MB, false, DS>(a, stream);
 }

@@ -229,3 +229,18 @@ def test_fused_efficientnet_b0_stream_split_bit_identical(net, nstreams):
         got = fused.forward_streams(x, streams)
     torch.cuda.synchronize()
     assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+
+
+def test_fused_efficientnet_b0_specialised_epilogues_bit_identical(net, monkeypatch):
+    """The specialised epilogues (projection convs: tq_epilogue.h emit4_linear_lut; the
+    expand engine's and depthwise kernel's forms) give the generic epilogues' logits bit for
+    bit (TQ_EPI_FAST=0, TQ_DW_FAST=0)."""
+    q, x = net
+    fused = tq_fuse.FusedEfficientNet(q)
+    with torch.no_grad():
+        fast = fused(x)
+        monkeypatch.setenv("TQ_EPI_FAST", "0")
+        monkeypatch.setenv("TQ_DW_FAST", "0")
+        generic = fused(x)
+    torch.cuda.synchronize()
+    assert torch.equal(fast.view(torch.int32), generic.view(torch.int32))

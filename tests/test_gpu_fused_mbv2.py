@@ -138,3 +138,17 @@ def test_fused_mobilenet_v2_stream_split_bit_identical(net, nstreams):
         got = fused.forward_streams(x, streams)
     torch.cuda.synchronize()
     assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+
+
+def test_fused_mobilenet_v2_specialised_epilogues_bit_identical(net, monkeypatch):
+    """The engines' specialised epilogues (projection convs: the linear form with one
+    table-served code output, tq_epilogue.h emit4_linear_lut; ReLU6 / ReLU forms elsewhere)
+    give the generic epilogue's logits bit for bit (TQ_EPI_FAST=0)."""
+    q, x = net
+    fused = tq_fuse.FusedMobileNetV2(q)
+    with torch.no_grad():
+        fast = fused(x)
+        monkeypatch.setenv("TQ_EPI_FAST", "0")
+        generic = fused(x)
+    torch.cuda.synchronize()
+    assert torch.equal(fast.view(torch.int32), generic.view(torch.int32))
