@@ -172,6 +172,29 @@ __device__ __forceinline__ void emit4_linear_lut(const ConvArgs& a, int64_t p, i
     *reinterpret_cast<int2*>(a.codes_a + p * a.cp_a + co + 4) = make_int2(0, 0);
 }
 
+// The swish form with one table-served code output and nothing else (EfficientNet-b0's
+// expand convs: no residual, no fp32 output, no second code output) of emit4_nhwc_res<true>.
+__device__ __forceinline__ void emit4_swish_lut(const ConvArgs& a, int64_t p, int co,
+                                                const int acc[4], const coef_t sc[4],
+                                                const coef_t sh[4], const uint16_t* lut_a) {
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = swish_f32(fold_acc(acc[i], sc[i], sh[i]));
+  uint32_t v[4];
+  lut_codes<4>(y, a.inv_a, a.maxv_a, a.fmt_a, false, lut_a, v);
+  *reinterpret_cast<int2*>(a.codes_a + p * a.cp_a + co) =
+      make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+  if (co + 4 == a.Cout && a.cp_a > a.Cout)
+    *reinterpret_cast<int2*>(a.codes_a + p * a.cp_a + co + 4) = make_int2(0, 0);
+}
+
+// 4 = emit4_swish_lut's form (the direct engine's swish instantiation picks it: swish_form)
+__host__ inline bool swish_lut_form(const ConvArgs& a) {
+  const char* env = getenv("TQ_EPI_FAST");
+  return !(env && atoi(env) == 0) && (a.Cout & 3) == 0 && !a.ds_x && !a.residual && !a.out &&
+         a.codes_a && a.lut_a > 0 && !a.codes_b;
+}
+
 // Epilogue form of a conv launch the engines specialise (0 = the generic emit4_nhwc(_res)):
 // 1 = ReLU with every code output from its table (emit4_relu_lut), 2 = the identity form
 // (emit4_identity), 3 = the linear form with one table-served code output (emit4_linear_lut;

@@ -78,7 +78,7 @@ struct DirCfg {
 // epilogue turns them into the identity (what the separate downsample conv would store) and
 // adds it where a residual read from HBM would go.
 // EPI: tq_epilogue.h epilogue_form (1 ReLU + code tables, 2 identity, 3 linear + one code
-// table; the host picks it)
+// table; the host picks it), 4 swish + one code table (SWISH only, swish_lut_form)
 template <int MB, bool FLUSH, bool DS, bool SWISH, int EPI = 0>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
@@ -430,6 +430,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
         emit4_identity(a, p, c4, acc4, psc, psh);
       else if constexpr (EPI == 3)
         emit4_linear_lut(a, p, c4, acc4, psc, psh, rv, lut_a);
+      else if constexpr (EPI == 4)
+        emit4_swish_lut(a, p, c4, acc4, psc, psh, lut_a);
       else
         emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
     }
@@ -466,6 +468,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
       emit4_identity(a, p, co, acc4, sc, sh);
     else if constexpr (EPI == 3)
       emit4_linear_lut(a, p, co, acc4, sc, sh, res[it], lut_a);  // (host: vec)
+    else if constexpr (EPI == 4)
+      emit4_swish_lut(a, p, co, acc4, sc, sh, lut_a);
     else if (vec)
       emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
@@ -745,6 +749,9 @@ hipError_t launch_conv2d_direct(const ConvArgs& a, int mb, hipStream_t stream) {
   if (a.relu == kActSwish) {  // swish epilogue (EfficientNet): 64-row tiles, no fused downsample
     if (a.ds_x || (a.Cout & 3)) return hipErrorInvalidValue;
     const bool flush = a.kc_steps > 0 && a.kc_steps < a.Kp / kKStep;
+    if (swish_lut_form(a))  // (the expand convs' codes-only form, EPI 4)
+      return flush ? launch_direct_cfg<1, true, false, true, 4>(a, stream)
+                   : launch_direct_cfg<1, false, false, true, 4>(a, stream);
     return flush ? launch_direct_cfg<1, true, false, true>(a, stream)
                  : launch_direct_cfg<1, false, false, true>(a, stream);
   }
