@@ -104,6 +104,8 @@ __device__ __forceinline__ void emit4_nhwc_res(const ConvArgs& a, int64_t p, int
 // emit4_nhwc_res for the ResNet executors' form -- ReLU, the code outputs served by their
 // tables (a.lut_a, and a.lut_b when codes_b) -- with that form's operations only: the same
 // values and stores without the runtime branches (and registers) of the other forms'.
+// RELU6: the ReLU6 form (MobileNet-V2's expand convs, epilogue_form 5).
+template <bool RELU6 = false>
 __device__ __forceinline__ void emit4_relu_lut(const ConvArgs& a, int64_t p, int co,
                                                const int acc[4], const coef_t sc[4],
                                                const coef_t sh[4], const float4 rv,
@@ -116,6 +118,7 @@ __device__ __forceinline__ void emit4_relu_lut(const ConvArgs& a, int64_t p, int
     if (a.residual || a.ds_x) y[i] += r[i];
     o[i] = y[i];
     y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+    if (RELU6) y[i] = y[i] < 6.0f ? y[i] : 6.0f;
     o[i] = o[i] != o[i] ? o[i] : y[i];
   }
   if (a.out)
@@ -197,8 +200,9 @@ __host__ inline bool swish_lut_form(const ConvArgs& a) {
 
 // Epilogue form of a conv launch the engines specialise (0 = the generic emit4_nhwc(_res)):
 // 1 = ReLU with every code output from its table (emit4_relu_lut), 2 = the identity form
-// (emit4_identity), 3 = the linear form with one table-served code output (emit4_linear_lut;
-// the direct engine only -- the others run 0 for it).  TQ_EPI_FAST=0 keeps the generic
+// (emit4_identity), 3 = the linear form with one table-served code output (emit4_linear_lut),
+// 5 = form 1 with ReLU6 (emit4_relu_lut<true>) -- 3 and 5 in the direct engine only, the
+// others run 0 for them.  TQ_EPI_FAST=0 keeps the generic
 // epilogue (tests, A/B).
 __host__ inline int epilogue_form(const ConvArgs& a) {
   const char* env = getenv("TQ_EPI_FAST");
@@ -207,6 +211,8 @@ __host__ inline int epilogue_form(const ConvArgs& a) {
     return 1;
   if (a.relu == 0 && a.out && !a.codes_a && !a.codes_b && !a.residual) return 2;
   if (a.relu == 0 && a.codes_a && a.lut_a > 0 && !a.codes_b) return 3;
+  if (a.relu == 2 && a.codes_a && a.lut_a > 0 && (a.codes_b == nullptr || a.lut_b > 0))
+    return 5;
   return 0;
 }
 

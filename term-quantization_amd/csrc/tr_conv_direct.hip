@@ -78,7 +78,8 @@ struct DirCfg {
 // epilogue turns them into the identity (what the separate downsample conv would store) and
 // adds it where a residual read from HBM would go.
 // EPI: tq_epilogue.h epilogue_form (1 ReLU + code tables, 2 identity, 3 linear + one code
-// table; the host picks it), 4 swish + one code table (SWISH only, swish_lut_form)
+// table, 5 ReLU6 + code tables; the host picks it), 4 swish + one code table (SWISH only,
+// swish_lut_form)
 template <int MB, bool FLUSH, bool DS, bool SWISH, int EPI = 0>
 __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvArgs a) {
   using C = DirCfg<MB>;
@@ -432,6 +433,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
         emit4_linear_lut(a, p, c4, acc4, psc, psh, rv, lut_a);
       else if constexpr (EPI == 4)
         emit4_swish_lut(a, p, c4, acc4, psc, psh, lut_a);
+      else if constexpr (EPI == 5)
+        emit4_relu_lut<true>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
       else
         emit4_nhwc_res<SWISH>(a, p, c4, acc4, psc, psh, rv, lut_a, lut_b);
     }
@@ -470,6 +473,8 @@ __global__ __launch_bounds__(kDirThreads, 2) void conv2d_tp_direct_kernel(ConvAr
       emit4_linear_lut(a, p, co, acc4, sc, sh, res[it], lut_a);  // (host: vec)
     else if constexpr (EPI == 4)
       emit4_swish_lut(a, p, co, acc4, sc, sh, lut_a);
+    else if constexpr (EPI == 5)
+      emit4_relu_lut<true>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else if (vec)
       emit4_nhwc_res<SWISH>(a, p, co, acc4, sc, sh, res[it], lut_a, lut_b);
     else
@@ -710,6 +715,9 @@ hipError_t launch_direct_mb(const ConvArgs& a, hipStream_t stream) {
   if (form == 3)
     return flush ? launch_direct_cfg<1, true, false, false, 3>(a, stream)
                  : launch_direct_cfg<1, false, false, false, 3>(a, stream);
+  if (form == 5)
+    return flush ? launch_direct_cfg<1, true, false, false, 5>(a, stream)
+                 : launch_direct_cfg<1, false, false, false, 5>(a, stream);
   return flush ? launch_direct_cfg<MB, true, DS>(a, stream)
                : launch_direct_cfg<MB, false, DS>(a, stream);
 }
