@@ -235,8 +235,12 @@ def cnn_fused(arch, steps, warmup, batch, dev, nstreams=2):
     if tp is not None:  # 1x1 convs: HBM-bound (algorithmic bytes per launch, fused _Conv)
         tp.update({"bound": "hbm", "mfma_frac": tp.pop("frac"), "frac": tp.pop("hbm_frac", None)})
     dom = max(kern, key=lambda k: kern[k]["share_of_step"])
-    return {"images_per_s": batch / tf, "ms_per_step": tf * 1e3, "batch": batch,
-            "streams": nstreams, "images_per_s_one_stream": batch / tf1,
+    # the executor's faster launch mode on this box (both are the same kernels and logits:
+    # test_fused_*_stream_split_bit_identical); both rates are reported
+    best, streams_used = (tf, nstreams) if tf <= tf1 else (tf1, 1)
+    return {"images_per_s": batch / best, "ms_per_step": best * 1e3, "batch": batch,
+            "streams": streams_used, "images_per_s_streams": batch / tf,
+            "images_per_s_one_stream": batch / tf1,
             "timing": "median of 3 loops of %d eager steps each" % steps,
             "dominant_kernel": dom, "kernels": kern}
 
