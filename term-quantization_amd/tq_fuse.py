@@ -300,14 +300,22 @@ class FusedResNet(nn.Module):
             r = []
             res.append(r)
             gens.append(self._steps(xc, None, r))
+        # TQ_STREAM_LAG=L: chunk j starts j * L launches late, so the streams run different
+        # layers side by side (A/B option; 0 = lockstep round-robin)
+        lag = int(os.environ.get("TQ_STREAM_LAG", "0"))
         live = list(range(len(gens)))
+        rnd = 0
         while live:
             nxt = []
             for j in live:
+                if rnd < j * lag:
+                    nxt.append(j)
+                    continue
                 with torch.cuda.stream(streams[j]):
                     if next(gens[j], StopIteration) is not StopIteration:
                         nxt.append(j)
             live = nxt
+            rnd += 1
         capturing = torch.cuda.is_current_stream_capturing()
         for s, xc, r in zip(streams, chunks, res):
             cur.wait_stream(s)
