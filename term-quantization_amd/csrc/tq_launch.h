@@ -207,6 +207,10 @@ bool conv_xp_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_xp(const ConvArgs& a, hipStream_t stream);
 bool conv_ring_eligible(const ConvArgs& a, int out_nhwc);
 hipError_t launch_conv2d_ring(const ConvArgs& a, hipStream_t stream);
+// MFMA Cout-64 pixel-ring engine (tr_conv_c64.hip): 3x3 stride-1 pad-1 64 -> 64 convs, ReLU
+// + table codes epilogue forms, NHWC out (ResNet-18 layer 1).
+bool conv_c64_eligible(const ConvArgs& a, int out_nhwc);
+hipError_t launch_conv2d_c64(const ConvArgs& a, hipStream_t stream);
 // MFMA row-strip engine (tr_conv_strip.hip): 3x3 stride-1 pad-1 convs with 64 -> 64 channels,
 // W % 8 == 0, W <= 56, kc_steps == 0, NHWC out (ResNet-18 layer 1).
 bool conv_strip_eligible(const ConvArgs& a, int out_nhwc);

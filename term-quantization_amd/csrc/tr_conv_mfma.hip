@@ -499,7 +499,9 @@ hipError_t launch_mfma_cfg(const ConvArgs& a, int out_nhwc, hipStream_t stream) 
 // 12 persistent pointwise (tr_conv_direct.hip: 1x1, K <= 3 K-steps; else the default).
 // 13 tap ring (tr_conv_ring.hip: 3x3/1 "same", Cp % 64 == 0, Wo <= 256; else the default).
 // 14 expand (tr_conv_xp.hip: 1x1/1, one or two K-steps, weights <= 64 KB; else the default).
-int conv_mfma_num_configs() { return 14; }
+// 15 Cout-64 pixel ring (tr_conv_c64.hip: 3x3/1 "same", 64 -> 64, ReLU + table codes; else the
+// default).
+int conv_mfma_num_configs() { return 15; }
 
 hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t stream) {
   if (a_in.P == 0 || a_in.Cout == 0) return hipSuccess;
@@ -545,6 +547,13 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   if ((cfg == 12 || (cfg < 0 && ring_on)) && conv_ring_eligible(a, out_nhwc))
     return launch_conv2d_ring(a, stream);
   if (cfg == 12) cfg = -1;
+  // Cout-64 pixel-ring engine: config 15, and the default for the layer-1 convs it takes
+  // (TQ_C64=0 / 1 forces it off / on; read per launch: tests switch it)
+  const char* c64 = getenv("TQ_C64");
+  const bool c64_on = c64 ? atoi(c64) == 1 : true;
+  if ((cfg == 14 || (cfg < 0 && c64_on)) && conv_c64_eligible(a, out_nhwc))
+    return launch_conv2d_c64(a, stream);
+  if (cfg == 14) cfg = -1;
   static const char* strip = getenv("TQ_STRIP");  // A/B override (tools only): 0 off
   if (cfg == 10 || (cfg < 0 && !(strip && atoi(strip) == 0))) {
     if (conv_strip_eligible(a, out_nhwc)) return launch_conv2d_strip(a, stream);

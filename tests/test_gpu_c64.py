@@ -1,0 +1,135 @@
+"""GPU parity of the Cout-64 pixel-ring engine (csrc/tr_conv_c64.hip, MFMA config 15).
+
+The engine sums the same exact integers as every other term-pair engine, so its outputs and
+emitted codes must be bit-identical to the VALU engine's (int16 codes, int32 sums, no fp32
+windows) on every shape and epilogue form it accepts: the ResNet-18 layer-1 convs (conv1:
+ReLU + codes; conv2: + residual, with and without the fp32 output; one or two code outputs),
+images smaller and larger than a tile (tiles crossing image boundaries, the widest halo W =
+63), every exactness-window setting, and few persistent workgroups (TQ_C64_GRID) so one
+workgroup walks many tiles through its pixel ring -- including a partial last tile."""
+import pytest
+import torch
+import torch.nn as nn
+
+import tq_native
+import tq_ops
+import tr_layer
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+C64 = 15  # MFMA config number of the Cout-64 pixel-ring engine
+
+
+def _run(codes, lay, hw, *, cfg, sc, sh, res=None, out=True, codes_a=True, codes_b=False,
+         fmt=torch.float16, kc_steps=0):
+    n = codes.shape[0]
+    o = torch.full((n, 64, hw, hw), float("nan"), device=DEV).contiguous(
+        memory_format=torch.channels_last) if out else None
+    ca = torch.full((n, hw, hw, 64), 7, dtype=torch.int16, device=DEV).to(fmt) \
+        if codes_a else None
+    cb = torch.full((n, hw, hw, 64), 7, dtype=torch.int16, device=DEV).to(fmt) \
+        if codes_b else None
+    tq_native.conv2d_termpair_fused(codes, lay.w_codes, 64, 3, 3, (1, 1), (1, 1), (1, 1),
+                                    hw, hw, out=o, ch_scale=sc, ch_shift=sh, residual=res,
+                                    relu=True, codes_a=ca,
+                                    quant_a=(0.05, 9, 3) if codes_a else None, codes_b=cb,
+                                    quant_b=(0.11, 9, 2) if codes_b else None, config=cfg,
+                                    kc_steps=kc_steps, kc_chunk=-1)
+    torch.cuda.synchronize()
+    return (None if o is None else o.view(torch.int32).cpu(),
+            None if ca is None else ca.float().cpu(),
+            None if cb is None else cb.float().cpu())
+
+
+def _case(hw, batch, seed):
+    torch.manual_seed(seed)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(DEV)
+    nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+    x = torch.relu(torch.randn(batch, 64, hw, hw, device=DEV)).to(
+        memory_format=torch.channels_last)
+    sc = (torch.rand(64, dtype=torch.float64, device=DEV) + 0.5) * 2e-4
+    sh = torch.randn(64, dtype=torch.float64, device=DEV) * 0.1
+    res = torch.randn(batch, 64, hw, hw, device=DEV).contiguous(
+        memory_format=torch.channels_last)
+    return conv, x, sc, sh, res
+
+
+def _layers(conv, x, monkeypatch):
+    monkeypatch.setenv("TQ_CONV_ENGINE", "valu")
+    lay_v = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    cv = torch.empty((x.shape[0], x.shape[2], x.shape[3], 64), dtype=torch.int16, device=DEV)
+    tq_native.act_encode(x, True, 0.02, 9, 3, cv)
+    monkeypatch.setenv("TQ_CONV_ENGINE", "mfma")
+    lay_m = tr_layer.TRConv2dLayer(conv, 9, 3, 9, 8, 12)
+    assert lay_m.engine == "mfma"
+    cm = torch.empty_like(cv, dtype=torch.float16)
+    tq_native.act_encode(x, True, 0.02, 9, 3, cm)
+    return lay_v, cv, lay_m, cm
+
+
+FORMS = {
+    "conv1": dict(out=False),                         # ReLU + codes (block conv1s)
+    "conv2_out": dict(res=True),                      # + residual + fp32 out (layer1.0.conv2)
+    "conv2_codes": dict(res=True, out=False),         # + residual, codes only (layer1.1.conv2)
+    "two_codes": dict(res=True, codes_b=True),        # a second code output
+    "out_only": dict(res=True, codes_a=False),        # fp32 output, no codes
+}
+
+
+@pytest.mark.parametrize("hw,batch", [
+    (56, 2),    # ResNet-18 layer 1 (12.25 tiles per image: tiles cross images)
+    (63, 32),   # the widest halo (W + 1 = 64)
+    (20, 8),    # images smaller than a tile: one tile spans 1.6 images
+    (7, 32),    # 49-pixel images
+])
+@pytest.mark.parametrize("grid", ["0", "3", "1"])
+def test_c64_bit_identical_to_valu(hw, batch, grid, monkeypatch):
+    conv, x, sc, sh, res = _case(hw, batch, seed=hw + batch)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    monkeypatch.setenv("TQ_C64_GRID", grid)
+    for form, kw in FORMS.items():
+        kw = dict(kw)
+        if kw.pop("res", False):
+            kw["res"] = res
+        ref = _run(cv, lay_v, hw, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
+        if ref[0] is not None:
+            assert not torch.isnan(ref[0].view(torch.float32)).any()
+        for kc in (lay_m.kc_steps, lay_m.kc_steps_nonneg, 5, 2, 1):
+            got = _run(cm, lay_m, hw, cfg=C64, sc=sc, sh=sh, kc_steps=kc, **kw)
+            for g, r in zip(got, ref):
+                assert (g is None and r is None) or torch.equal(g, r), (form, kc)
+
+
+def test_c64_partial_last_tile(monkeypatch):
+    """N*H*W = 3 * 56^2 = 9408 = 36.75 tiles: the last tile's upper 64 pixels (two waves'
+    blocks) are past the tensor -- their taps read the zero pixel, their stores are dropped;
+    the guard rows of the output buffers stay untouched."""
+    conv, x, sc, sh, res = _case(56, 3, seed=5)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, 56, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16)
+    for grid in ("0", "2", "37"):
+        monkeypatch.setenv("TQ_C64_GRID", grid)
+        got = _run(cm, lay_m, 56, cfg=C64, sc=sc, sh=sh, res=res, kc_steps=lay_m.kc_steps)
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), grid
+
+
+def test_c64_is_the_layer1_default(monkeypatch):
+    """With no config the dispatcher picks the engine for the layer-1 forms (and TQ_C64=0
+    turns it off): same bits either way."""
+    conv, x, sc, sh, res = _case(56, 2, seed=9)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, 56, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16)
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TQ_C64", flag)
+        got = _run(cm, lay_m, 56, cfg=0, sc=sc, sh=sh, res=res, kc_steps=lay_m.kc_steps)
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), flag
+
+
+def test_c64_ineligible_shapes_fall_back(monkeypatch):
+    """Forms and shapes the engine does not take (N*H*W % 32 != 0, no ReLU, a stride) run the
+    default engine under config 15, with the same bits as the VALU engine."""
+    conv, x, sc, sh, res = _case(9, 3, seed=13)  # 243 pixels
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, 9, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16)
+    got = _run(cm, lay_m, 9, cfg=C64, sc=sc, sh=sh, res=res, kc_steps=lay_m.kc_steps)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--no-out", action="store_true", help="no fp32 output (codes only)")
     ap.add_argument("--shape", default=None, help="cin,cout,k,stride,hin instead of --layer")
     ap.add_argument("--no-relu", action="store_true", help="no activation (signed codes)")
+    ap.add_argument("--nonneg", action="store_true",
+                    help="exactness windows for non-negative codes (the fused executor's)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -59,8 +61,9 @@ def main():
         codes_a=ca, quant_a=q if ca is not None else None, codes_b=cb,
         quant_b=q if cb is not None else None,
         workspace=None if layer.engine == "mfma" else ws,
-        split_k=args.split, config=args.config, kc_steps=layer.kc_steps,
-        kc_chunk=getattr(layer, "kc_chunk", -1))
+        split_k=args.split, config=args.config,
+        kc_steps=layer.kc_steps_nonneg if args.nonneg else layer.kc_steps,
+        kc_chunk=getattr(layer, "kc_chunk_nonneg" if args.nonneg else "kc_chunk", -1))
     t = time_fn(fn, args.iters)
     mac = args.batch * cout * ho * ho * cin * k * k
     print("layer %d cfg %d split %d: %.1f us  %.1f TMAC/s" % (args.layer, args.config,
