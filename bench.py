@@ -104,17 +104,20 @@ def launch_plan(gpus, env):
     return ("run", gpus)
 
 
-def spawn_ranks(argv, n, dry):
-    """Start ranks 0..n-1 as fresh processes (this one has not touched the GPU: only
-    torch.cuda.device_count(), which does not initialise it on this image), one per GPU,
-    rendezvous on 127.0.0.1; return non-zero if any rank fails."""
+def spawn_ranks(argv, n, dry, timeout_s=None, poll_s=0.2):
+    """Start ranks 0..n-1 as fresh processes, one per GPU, rendezvous on 127.0.0.1; return
+    non-zero if any rank fails.  This process never touches torch.cuda (not even
+    device_count(), which falls back to hipGetDeviceCount when amdsmi fails and would then
+    initialise HIP in the parent of every rank): each rank checks the visible GPU count
+    itself (check_world).  The children are polled: when one exits non-zero the others are
+    terminated (a rank stuck in init or a collective would otherwise block until the process
+    group times out), and all of them when the overall time limit (TQ_BENCH_SPAWN_TIMEOUT
+    seconds, default 3600) passes."""
     import socket
     import subprocess
-    if not dry:
-        have = torch.cuda.device_count()
-        if have < n:
-            print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, have), file=sys.stderr)
-            return 2
+    import time
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("TQ_BENCH_SPAWN_TIMEOUT", "3600"))
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -124,8 +127,43 @@ def spawn_ranks(argv, n, dry):
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
                                       env=env))
-    rcs = [p.wait() for p in procs]
-    return 0 if all(rc == 0 for rc in rcs) else 1
+    t_end = time.monotonic() + timeout_s
+    failed = False
+    while True:
+        rcs = [p.poll() for p in procs]
+        if any(rc not in (None, 0) for rc in rcs):
+            failed = True
+            print("bench.py: a rank exited with %s; stopping the others" %
+                  [rc for rc in rcs if rc not in (None, 0)][0], file=sys.stderr)
+            break
+        if all(rc == 0 for rc in rcs):
+            return 0
+        if time.monotonic() > t_end:
+            failed = True
+            print("bench.py: ranks still running after %.0f s; stopping them" % timeout_s,
+                  file=sys.stderr)
+            break
+        time.sleep(poll_s)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return 1 if failed else 0
+
+
+def check_world(world, local):
+    """A rank's own check that its GPU exists (spawn_ranks leaves the count to the ranks)."""
+    have = torch.cuda.device_count()
+    if local >= have or world > have:
+        print("bench.py: world size %d (local rank %d) but only %d GPU(s) visible" %
+              (world, local, have), file=sys.stderr)
+        return False
+    return True
 
 
 class KernelTimer(object):
@@ -373,6 +411,8 @@ def main(argv=None):
         return 0
     os.environ["TQ_CONV_ENGINE"] = args.engine
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not check_world(world, local):
+        return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = True  # MIOpen picks its fastest stem-conv solver once

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kSeThreads) void se_gate_kernel(SeGateArgs a) {
   for (int c = tid; c < a.Cpr; c += kSeThreads)
     vx[c] = c < a.C ? tr_value_g1_inv(xin[c], a.inv_r, a.maxv_r, a.k_r) : 0;
   __syncthreads();
-  // reduce conv: output j by wave j % 4, its lanes along the input channels
+  // reduce conv: output j by wave j % 16, its lanes along the input channels
   for (int j = wave; j < a.Cse; j += kSeThreads / 64) {
     const int32_t* w = a.w_r + (int64_t)j * a.Cpr;
     // kSeU independent loads in flight per lane (the loop is paced by L2 latency)

@@ -549,8 +549,11 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   if (cfg == 12) cfg = -1;
   // Cout-64 pixel-ring engine: config 15, and the default for the layer-1 convs it takes
   // (TQ_C64=0 / 1 forces it off / on; read per launch: tests switch it)
+  // (its epilogues are all specialised ReLU + table forms: TQ_EPI_FAST=0, the generic-epilogue
+  // A/B, leaves these convs to the strip / direct engines)
   const char* c64 = getenv("TQ_C64");
-  const bool c64_on = c64 ? atoi(c64) == 1 : true;
+  const char* epi_fast = getenv("TQ_EPI_FAST");
+  const bool c64_on = c64 ? atoi(c64) == 1 : !(epi_fast && atoi(epi_fast) == 0);
   if ((cfg == 14 || (cfg < 0 && c64_on)) && conv_c64_eligible(a, out_nhwc))
     return launch_conv2d_c64(a, stream);
   if (cfg == 14) cfg = -1;

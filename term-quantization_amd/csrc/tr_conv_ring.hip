@@ -743,15 +743,16 @@ hipError_t launch_ring_fast(const ConvArgs& a, int R, int64_t ptc, int64_t grid,
 }
 
 // the specialised epilogue form (the kernel's FAST): 1 = ReLU + fp16 codes_a (+ codes_b) each
-// served by a code table; 2 = ReLU + fp32 output, no codes (TQ_EPI_FAST=0: generic only); 0
+// served by a code table; 2 = ReLU + fp32 output, no codes; 0 = the generic emit4_nhwc_res
+// (every form with TQ_EPI_FAST=0)
 bool ring_codes_form(const ConvArgs& a) {
   return a.relu == 1 && a.codes_a != nullptr && a.lut_a > 0 && a.fmt_a == kCodesF16 &&
          (a.codes_b == nullptr || (a.lut_b > 0 && a.fmt_b == kCodesF16));
 }
 int ring_epilogue_form(const ConvArgs& a) {
-  if (ring_codes_form(a)) return 1;
   const char* v = getenv("TQ_EPI_FAST");
   if (v && atoi(v) == 0) return 0;
+  if (ring_codes_form(a)) return 1;
   return a.relu == 1 && a.out != nullptr && a.codes_a == nullptr && a.codes_b == nullptr ? 2 : 0;
 }
 

@@ -259,8 +259,10 @@ bool conv_xp_eligible(const ConvArgs& a, int out_nhwc) {
 template <int NKS>
 hipError_t launch_xp_nks(const ConvArgs& a, hipStream_t stream) {
   // (the two-K-step instantiations of the fast forms spill at 4 waves per SIMD)
-  const bool fast = NKS == 1 && a.out == nullptr && a.codes_a != nullptr &&
-                    a.codes_b == nullptr && a.lut_a > 0;
+  // (TQ_EPI_FAST=0: the generic epilogue, as every engine's specialised forms)
+  const char* env = getenv("TQ_EPI_FAST");
+  const bool fast = !(env && atoi(env) == 0) && NKS == 1 && a.out == nullptr &&
+                    a.codes_a != nullptr && a.codes_b == nullptr && a.lut_a > 0;
   if constexpr (NKS == 1) {
     if (fast && a.relu == kActSwish) return launch_xp_cfg<NKS, true, 3>(a, stream);
     if (fast && a.relu == 2) return launch_xp_cfg<NKS, false, 2>(a, stream);

@@ -370,14 +370,17 @@ class TRLSTMLayer(nn.Module):
     the library LSTM, MIOpen on the GPU).
 
     ``termpair=True`` (the default for CUDA inputs) computes the same function with layer 0
-    on the term-pair kernels: its input projection over all time
-    steps is one exact term-pair GEMM, TR(emb) TR(W_ih)^T + b_ih, and so is the first step's
-    recurrent projection TR(h0) TR(W_hh)^T + b_hh (both operands term-revealed); later steps
-    multiply the fp32 state by the TR'd W_hh (hipBLASLt) and one HIP kernel per step applies
-    the gates (tq_lstm_cell_f32).  Layers >= 1 (weights untouched by the reference) run the
-    library LSTM on their quantized initial state.  fp32 results equal the reference
-    composition to rounding (tests/test_gpu_lstm.py) and run the LSTM-650 chunk 18 % faster
-    than MIOpen's LSTM (193 k vs 164 k tokens/s, profiles/r02l_d4.jsonl)."""
+    on the term-pair kernels: its input projection over all time steps is one exact
+    term-pair GEMM, TR(emb) TR(W_ih)^T + b_ih (both operands term-revealed).  The recurrences
+    then run as fused HIP step kernels launched from C++: for a 2-layer LSTM (LSTM-650) both
+    layers in wavefront order from ONE ``tq_lstm_seq2_f32`` call (T + 1 launches of
+    ``lstm_step2_kernel``: launch s runs layer 0's step s and layer 1's step s - 1, layer 1
+    computing x_t W_ih^T inside its step); ``TQ_LSTM_WAVE=0`` runs one ``tq_lstm_seq_f32`` call
+    per layer (T launches each), ``TQ_LSTM_SEQ=0`` the per-step hipBLASLt GEMM + one
+    ``tq_lstm_cell_f32`` launch per step.  Layers >= 1 keep the reference's untouched weights
+    and their quantized initial state.  fp32 results equal the reference composition to
+    rounding, per log-prob (tests/test_gpu_lstm.py); the LSTM-650 chunk runs at 459-481 k
+    tokens/s on the wavefront path vs 164-179 k for MIOpen's LSTM (bench d4)."""
 
     def __init__(self, lstm_layer, data_bits=8, data_terms=4, weight_bits=8,
                  group_size=1, num_terms=8, termpair=True):

@@ -41,3 +41,50 @@ def test_spawned_world_size_equals_gpus():
     lines = [json.loads(l) for l in r.stdout.strip().splitlines()]
     assert sorted(d["rank"] for d in lines) == [0, 1, 2]
     assert all(d["world_size"] == 3 and d["local_rank"] == d["rank"] for d in lines)
+
+
+def test_spawn_parent_never_initialises_hip():
+    """The self-spawning parent never calls into torch.cuda (device_count() can initialise HIP
+    through hipGetDeviceCount): with every torch.cuda entry point replaced by one that raises,
+    spawn_ranks still starts and reaps its (dry) ranks."""
+    code = """
+import sys, torch
+sys.path.insert(0, %r)
+def boom(*a, **k):
+    raise AssertionError("torch.cuda touched in the parent")
+for name in ("device_count", "is_available", "init", "set_device", "current_device",
+             "synchronize", "get_device_properties"):
+    setattr(torch.cuda, name, boom)
+torch._C._cuda_getDeviceCount = boom
+import bench
+sys.exit(bench.main(["--gpus", "2", "--dry-launch"]))
+""" % ROOT
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert sorted(json.loads(l)["rank"] for l in r.stdout.strip().splitlines()) == [0, 1]
+
+
+def test_spawn_stops_the_other_ranks_when_one_fails(tmp_path):
+    """A rank that fails makes spawn_ranks terminate the rest (instead of waiting for a
+    collective's timeout) and return non-zero; an overall time limit stops hung ranks."""
+    import time
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\\n"
+                      "r = int(os.environ['RANK'])\\n"
+                      "if r == 1: sys.exit(3)\\n"
+                      "time.sleep(600)\\n")
+    orig = bench.os.path.abspath
+    bench.os.path.abspath = lambda p: str(script) if p == bench.__file__ else orig(p)
+    try:
+        t0 = time.monotonic()
+        assert bench.spawn_ranks([], 3, True) != 0
+        assert time.monotonic() - t0 < 60
+        script.write_text("import time\\ntime.sleep(600)\\n")
+        t0 = time.monotonic()
+        assert bench.spawn_ranks([], 2, True, timeout_s=2) != 0
+        assert time.monotonic() - t0 < 60
+    finally:
+        bench.os.path.abspath = orig
