@@ -48,10 +48,25 @@
 //   LDS = weights [64][73 x 16 B] | ring [640][128 B] | zero pixel (128 B) | code tables
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "tq_device.h"
 #include "tq_epilogue.h"
 #include "tq_launch.h"
 #include "tq_mfma.h"
+
+#ifndef C64_AB
+#define C64_AB 0  // timing-only ablation builds (tools/variant1.sh); 0 = the product kernel
+#endif
+#ifndef C64_PF
+#define C64_PF 1  // substeps of fragment prefetch (1 or 2)
+#endif
+#ifndef C64_PRIO
+#define C64_PRIO 0  // 1: s_setprio 1 for waves 4-7, 2: for waves 0-3 (A/B builds)
+#endif
+#ifndef C64_STAGGER
+#define C64_STAGGER 1  // 0: every wave runs its epilogue right after its MFMAs (A/B builds)
+#endif
 
 namespace tq {
 
@@ -107,7 +122,7 @@ constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past every buffer thi
 // RES: fp32 residual input; OUT: fp32 output; NCODES: code outputs (each from its code table,
 // ReLU form); FLUSH: int32 exactness windows every kc_steps taps.
 template <bool RES, bool OUT, int NCODES, bool FLUSH>
-__global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, int ntiles) {
+__global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, int nblk) {
   extern __shared__ __attribute__((aligned(16))) u32x4 c64_lds[];
   unsigned char* lb = reinterpret_cast<unsigned char*>(c64_lds);
   const uint32_t lds0 =
@@ -117,13 +132,15 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31;
   const int hh = lane >> 5;
-  const bool late = wave >= 4;  // waves 4-7: epilogue deferred by one tile
+  const bool late = C64_STAGGER && wave >= 4;  // waves 4-7: epilogue deferred by one tile
 
   const int G = gridDim.x;
   const int g = xcd_remap(blockIdx.x, G);
-  const int t_begin = (int)((int64_t)g * ntiles / G);
-  const int t_end = (int)((int64_t)(g + 1) * ntiles / G);
-  if (t_begin >= t_end) return;  // (uniform: before any barrier)
+  // this workgroup's pixels [pb0, pe): an equal share of the 32-pixel blocks, walked as
+  // 256-pixel tiles from pb0 (the last tile may hold fewer blocks: its idle waves skip it)
+  const int pb0 = (int)((int64_t)g * nblk / G) * 32;
+  const int pe = (int)((int64_t)(g + 1) * nblk / G) * 32;
+  if (pb0 >= pe) return;  // (uniform: before any barrier)
 
   const int P = (int)a.P;  // the launcher checks P * 256 < 2^31
   const char* __restrict__ xb = reinterpret_cast<const char*>(a.x);
@@ -142,7 +159,7 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
   };
 
   // ---- prologue: the first tile's window, the weights, the zero pixel, the code tables
-  const int p_first = t_begin * kC64Tile;
+  const int p_first = pb0;
 #pragma unroll
   for (int i = 0; i < kC64ProloguePieces / 8; ++i)
     issue_piece(p_first - kC64Halo + 8 * (wave * (kC64ProloguePieces / 8) + i));
@@ -176,6 +193,8 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
 
   TQ_WAIT_VM(0);
   __syncthreads();  // weights, ring window, zero pixel, tables visible
+  if (C64_PRIO == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (C64_PRIO == 2 && wave < 4) __builtin_amdgcn_s_setprio(1);
 
   // B (weight) fragment base: row r32 of channel block 0, unit hh; + 32 rows for block 1,
   // + (8 t + 2 k) units for tap t, substep k -- all immediate offsets
@@ -191,7 +210,7 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
   auto load_res = [&](int pt) __attribute__((always_inline)) {
     if constexpr (RES) {
       const int pb = pt + 32 * wave;
-      const uint32_t vf = pb < P ? (uint32_t)(((pb + 4 * hh) * 64 + r32) * 4) : kOob;
+      const uint32_t vf = pb < pe ? (uint32_t)(((pb + 4 * hh) * 64 + r32) * 4) : kOob;
       c64_for<0, 2>([&](auto nbc) __attribute__((always_inline)) {
         constexpr int nb = decltype(nbc)::value;
         c64_for<0, 16>([&](auto rc) __attribute__((always_inline)) {
@@ -206,8 +225,12 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
 
   // epilogue of the wave's 32 pixels of tile pt from acc / acci and rv
   auto epilogue = [&](int pt) __attribute__((always_inline)) {
+    if (C64_AB == 1) {  // timing only: no epilogue (sums kept live)
+      asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][15]));
+      return;
+    }
     const int pb = pt + 32 * wave;
-    const bool okb = pb < P;
+    const bool okb = pb < pe;
     const uint32_t vf = okb ? (uint32_t)(((pb + 4 * hh) * 64 + r32) * 4) : kOob;
     const uint32_t vc = okb ? (uint32_t)(((pb + 4 * hh) * 64 + r32) * 2) : kOob;
     c64_for<0, 2>([&](auto nbc) __attribute__((always_inline)) {
@@ -215,8 +238,12 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
       c64_for<0, 16>([&](auto rc) __attribute__((always_inline)) {
         constexpr int r = decltype(rc)::value;
         constexpr uint32_t pix = 8 * (r >> 2) + (r & 3);
-        const int iacc = FLUSH ? acci[nb][r] : (int)acc[nb][r];
-        float y = fold_acc(iacc, (coef_t)sc[nb], (coef_t)sh[nb]);
+        // (without int32 windows the fp32 sum is an exact integer: converted to fp64
+        // directly, the same value fold_acc gets through int32)
+        float y = FLUSH || TQ_EPI_F32
+                      ? fold_acc(FLUSH ? acci[nb][r] : (int)acc[nb][r], (coef_t)sc[nb],
+                                 (coef_t)sh[nb])
+                      : (float)((double)acc[nb][r] * sc[nb] + sh[nb]);
         if constexpr (RES) y += rv[nb][r];
         float o = y;
         y = y > 0.0f ? y : 0.0f;
@@ -241,103 +268,127 @@ __global__ __launch_bounds__(kC64Threads) void conv2d_tp_c64_kernel(ConvArgs a, 
   constexpr int kStores = 32 * ((OUT ? 1 : 0) + NCODES);
   constexpr int kWaitYoung = kStores < 63 ? kStores : 63;
 
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int p0 = tile * kC64Tile;
-    if (tile != t_begin) {
-      // the early waves' DMA of this tile's new pixels (issued at the top of the previous
-      // tile; younger than it: that tile's epilogue stores -- and its residual loads, which
-      // the epilogue already waited for) has landed; the barrier publishes it and frees the
-      // slots of the tile before last
-      if (!late) TQ_WAIT_VM(kWaitYoung);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    if (!late && tile + 1 < t_end) {
-#pragma unroll
-      for (int i = 0; i < kC64TilePieces / 4; ++i)
-        issue_piece(p0 + kC64Tile + kC64Halo + 8 * (wave * (kC64TilePieces / 4) + i));
-    }
-    if (late && tile != t_begin) epilogue(p0 - kC64Tile);
+  // the tile loop, compiled once per role: with one body for both, the compiler's wait-count
+  // analysis merged the roles' paths (a late wave's residual loads still in flight where an
+  // early wave reloads them) and drained vmcnt(0) -- the DMA just issued -- every tile
+  // (and the first tile is peeled: a loop-carried "first tile?" test left a path on which a late
+  // wave's residual loads were still in flight where it reloads them -- vmcnt(0) again)
+  auto run = [&](auto late_c) __attribute__((always_inline)) {
+    constexpr bool LATE = decltype(late_c)::value;
+    auto body = [&](auto first_c, int p0) __attribute__((always_inline)) {
+      constexpr bool FIRST = decltype(first_c)::value;
+      const bool act = p0 + 32 * wave < pe;  // this wave's block is in the range (uniform)
+      if (!FIRST) {
+        // the early waves' DMA of this tile's new pixels (issued at the top of the previous
+        // tile; younger than it: that tile's epilogue stores -- and its residual loads, which
+        // the epilogue already waited for) has landed; the barrier publishes it and frees the
+        // slots of the tile before last
+        if (!LATE) TQ_WAIT_VM(kWaitYoung);
+        if (C64_AB != 4) __builtin_amdgcn_s_barrier();  // (4: timing only, no barrier)
+        asm volatile("" ::: "memory");
+      }
+      if (C64_AB != 3 && !LATE && p0 + kC64Tile < pe) {  // (3: timing only, no ring refill)
+  #pragma unroll
+        for (int i = 0; i < kC64TilePieces / 4; ++i)
+          issue_piece(p0 + kC64Tile + kC64Halo + 8 * (wave * (kC64TilePieces / 4) + i));
+      }
+      if (LATE && !FIRST) epilogue(p0 - kC64Tile);  // (a wave idles in the last tile only)
+      if (!act) return;  // (no barrier follows: this is the range's last tile)
 
-    // ---- tap addresses of the lane's A row (pixel p0 + 32 wave + r32): ring slot of the tap's
-    // input pixel (or the zero pixel), XOR-swizzled, unit hh applied
-    uint32_t xa[kC64Taps];
-    {
-      const int p = p0 + 32 * wave + r32;
-      const bool okp = p < P;
-      const int img = okp ? p / HW : 0;
-      const int rem = p - img * HW;
-      const int y = rem / a.W;
-      const int x = rem - y * a.W;
-      int sb = (p0 % kC64Ring) + 32 * wave + r32;
-      sb = sb >= kC64Ring ? sb - kC64Ring : sb;
-#pragma unroll
-      for (int t = 0; t < kC64Taps; ++t) {
-        const int dy = t / 3 - 1, dx = t % 3 - 1;
-        const bool ok = okp && (unsigned)(y + dy) < (unsigned)a.H &&
-                        (unsigned)(x + dx) < (unsigned)a.W;
-        int s = sb + dy * a.W + dx;
-        s = s < 0 ? s + kC64Ring : (s >= kC64Ring ? s - kC64Ring : s);
-        const uint32_t in = (uint32_t)(kC64RingOff + s * 128 + ((s >> 1) & 7) * 16);
-        xa[t] = (ok ? in : (uint32_t)kC64ZeroOff) ^ (uint32_t)(hh * 16);
-      }
-    }
-    load_res(p0);
-
-    // ---- main loop: 36 substeps, fragments one substep ahead
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[nb][r] = 0.0f;
-        if (FLUSH) acci[nb][r] = 0;
-      }
-    half8 fa[2], fb[2][2];
-    fa[0] = c64_frag(lds0 + xa[0]);
-    fb[0][0] = c64_frag(wbase);
-    fb[0][1] = c64_frag(wbase + 32 * kC64WPitch);
-    int since = 0;
-    c64_for<0, kC64Sub>([&](auto sc_) __attribute__((always_inline)) {
-      constexpr int s = decltype(sc_)::value;
-      constexpr int t = s / 4, k = s % 4, cb = s & 1, nx = cb ^ 1;
-      if constexpr (s + 1 < kC64Sub) {
-        constexpr int t1 = (s + 1) / 4, k1 = (s + 1) % 4;
-        // (xa ^ 32 k: the unit of substep k in the swizzled slot)
-        fa[nx] = c64_frag(lds0 + (xa[t1] ^ (uint32_t)(32 * k1)));
-        fb[nx][0] = c64_frag(wbase + (uint32_t)(128 * t1 + 32 * k1));
-        fb[nx][1] = c64_frag(wbase + (uint32_t)(32 * kC64WPitch + 128 * t1 + 32 * k1));
-      }
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[cb], fb[cb][0], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[cb], fb[cb][1], acc[1], 0, 0, 0);
-      // keep the order: the next substep's reads, then this substep's MFMAs
-      if constexpr (s + 1 < kC64Sub) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      if constexpr (FLUSH && k == 3 && t + 1 < kC64Taps) {
-        if (++since == a.kc_steps) {
-          since = 0;
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              acci[nb][r] += (int)acc[nb][r];
-              acc[nb][r] = 0.0f;
-            }
+      // ---- tap addresses of the lane's A row (pixel p0 + 32 wave + r32): ring slot of the tap's
+      // input pixel (or the zero pixel), XOR-swizzled, unit hh applied
+      uint32_t xa[kC64Taps];
+      {
+        const int p = p0 + 32 * wave + r32;
+        const bool okp = p < P;
+        const int img = okp ? p / HW : 0;
+        const int rem = p - img * HW;
+        const int y = rem / a.W;
+        const int x = rem - y * a.W;
+        int sb = (p0 % kC64Ring) + 32 * wave + r32;
+        sb = sb >= kC64Ring ? sb - kC64Ring : sb;
+  #pragma unroll
+        for (int t = 0; t < kC64Taps; ++t) {
+          const int dy = t / 3 - 1, dx = t % 3 - 1;
+          const bool ok = okp && (unsigned)(y + dy) < (unsigned)a.H &&
+                          (unsigned)(x + dx) < (unsigned)a.W;
+          int s = sb + dy * a.W + dx;
+          s = s < 0 ? s + kC64Ring : (s >= kC64Ring ? s - kC64Ring : s);
+          const uint32_t in = (uint32_t)(kC64RingOff + s * 128 + ((s >> 1) & 7) * 16);
+          xa[t] = (ok ? in : (uint32_t)kC64ZeroOff) ^ (uint32_t)(hh * 16);
         }
       }
-    });
-    if constexpr (FLUSH) {
-#pragma unroll
+      load_res(p0);
+
+      // ---- main loop: 36 substeps, fragments one substep ahead
+  #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acci[nb][r] += (int)acc[nb][r];
-    }
-    if (!late) epilogue(p0);
-  }
-  if (late) epilogue((t_end - 1) * kC64Tile);
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[nb][r] = 0.0f;
+          if (FLUSH) acci[nb][r] = 0;
+        }
+      constexpr int NF = C64_PF + 1;  // fragment buffers
+      half8 fa[NF], fb[NF][2];
+      auto read_frags = [&](auto sc_, int buf) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc_)::value;
+        constexpr int t = s / 4, k = s % 4;
+        // (xa ^ 32 k: the unit of substep k in the swizzled slot)
+        fa[buf] = c64_frag(lds0 + (xa[t] ^ (uint32_t)(32 * k)));
+        fb[buf][0] = c64_frag(wbase + (uint32_t)(128 * t + 32 * k));
+        fb[buf][1] = c64_frag(wbase + (uint32_t)(32 * kC64WPitch + 128 * t + 32 * k));
+      };
+      c64_for<0, C64_PF>([&](auto sc_) __attribute__((always_inline)) {
+        read_frags(sc_, decltype(sc_)::value);
+      });
+      int since = 0;
+      c64_for<0, kC64Sub>([&](auto sc_) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc_)::value;
+        constexpr int t = s / 4, k = s % 4, cb = s % NF;
+        if constexpr (s + C64_PF < kC64Sub) read_frags(c64_ic<s + C64_PF>{}, (s + C64_PF) % NF);
+  #if C64_AB == 2  // timing only: no MFMA (fragments kept live)
+        asm volatile("" ::"v"(fa[cb]), "v"(fb[cb][0]), "v"(fb[cb][1]));
+  #else
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[cb], fb[cb][0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[cb], fb[cb][1], acc[1], 0, 0, 0);
+  #endif
+        // keep the order: the prefetched substep's reads, then this substep's MFMAs
+        if constexpr (s + C64_PF < kC64Sub) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if constexpr (FLUSH && k == 3 && t + 1 < kC64Taps) {
+          if (++since == a.kc_steps) {
+            since = 0;
+  #pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                acci[nb][r] += (int)acc[nb][r];
+                acc[nb][r] = 0.0f;
+              }
+          }
+        }
+      });
+      if constexpr (FLUSH) {
+  #pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acci[nb][r] += (int)acc[nb][r];
+      }
+      if (!LATE) epilogue(p0);
+    };
+    body(std::true_type{}, pb0);
+    for (int p0 = pb0 + kC64Tile; p0 < pe; p0 += kC64Tile) body(std::false_type{}, p0);
+    const int p_last = pb0 + (pe - 1 - pb0) / kC64Tile * kC64Tile;
+    if (LATE && p_last + 32 * wave < pe) epilogue(p_last);
+  };
+  if (late)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 }
 
 template <bool RES, bool OUT, int NCODES, bool FLUSH>
-hipError_t launch_c64(const ConvArgs& a, int grid, int ntiles, size_t lds, hipStream_t stream) {
+hipError_t launch_c64(const ConvArgs& a, int grid, int nblk, size_t lds, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
@@ -347,24 +398,24 @@ hipError_t launch_c64(const ConvArgs& a, int grid, int ntiles, size_t lds, hipSt
     attr_set = true;
   }
   conv2d_tp_c64_kernel<RES, OUT, NCODES, FLUSH>
-      <<<dim3((unsigned)grid), kC64Threads, lds, stream>>>(a, ntiles);
+      <<<dim3((unsigned)grid), kC64Threads, lds, stream>>>(a, nblk);
   return hipGetLastError();
 }
 
 template <bool RES, bool OUT, int NCODES>
-hipError_t launch_c64_flush(const ConvArgs& a, int grid, int ntiles, size_t lds,
+hipError_t launch_c64_flush(const ConvArgs& a, int grid, int nblk, size_t lds,
                             hipStream_t stream) {
   return a.kc_steps > 0 && a.kc_steps < kC64Taps
-             ? launch_c64<RES, OUT, NCODES, true>(a, grid, ntiles, lds, stream)
-             : launch_c64<RES, OUT, NCODES, false>(a, grid, ntiles, lds, stream);
+             ? launch_c64<RES, OUT, NCODES, true>(a, grid, nblk, lds, stream)
+             : launch_c64<RES, OUT, NCODES, false>(a, grid, nblk, lds, stream);
 }
 
 template <bool RES, bool OUT>
-hipError_t launch_c64_codes(const ConvArgs& a, int grid, int ntiles, size_t lds,
+hipError_t launch_c64_codes(const ConvArgs& a, int grid, int nblk, size_t lds,
                             hipStream_t stream) {
-  if (a.codes_b) return launch_c64_flush<RES, OUT, 2>(a, grid, ntiles, lds, stream);
-  if (a.codes_a) return launch_c64_flush<RES, OUT, 1>(a, grid, ntiles, lds, stream);
-  return launch_c64_flush<RES, OUT, 0>(a, grid, ntiles, lds, stream);
+  if (a.codes_b) return launch_c64_flush<RES, OUT, 2>(a, grid, nblk, lds, stream);
+  if (a.codes_a) return launch_c64_flush<RES, OUT, 1>(a, grid, nblk, lds, stream);
+  return launch_c64_flush<RES, OUT, 0>(a, grid, nblk, lds, stream);
 }
 
 int64_t c64_lds_bytes(const ConvArgs& a) { return kC64LutOff + conv_lut_bytes(a); }
@@ -388,17 +439,17 @@ bool conv_c64_eligible(const ConvArgs& a, int out_nhwc) {
 
 hipError_t launch_conv2d_c64(const ConvArgs& a, hipStream_t stream) {
   if (!conv_c64_eligible(a, 1)) return hipErrorInvalidValue;
-  const int ntiles = (int)((a.P + kC64Tile - 1) / kC64Tile);
+  const int nblk = (int)(a.P / 32);  // 32-pixel blocks, split evenly over the workgroups
   int grid = device_cus();
   const char* genv = getenv("TQ_C64_GRID");  // tests: fewer workgroups, longer tile runs
   if (genv && atoi(genv) > 0) grid = atoi(genv);
-  if (grid > ntiles) grid = ntiles;
+  if (grid > (nblk + 7) / 8) grid = (nblk + 7) / 8;  // at least a full tile each
   const size_t lds = (size_t)c64_lds_bytes(a);
   if (a.residual)
-    return a.out ? launch_c64_codes<true, true>(a, grid, ntiles, lds, stream)
-                 : launch_c64_codes<true, false>(a, grid, ntiles, lds, stream);
-  return a.out ? launch_c64_codes<false, true>(a, grid, ntiles, lds, stream)
-               : launch_c64_codes<false, false>(a, grid, ntiles, lds, stream);
+    return a.out ? launch_c64_codes<true, true>(a, grid, nblk, lds, stream)
+                 : launch_c64_codes<true, false>(a, grid, nblk, lds, stream);
+  return a.out ? launch_c64_codes<false, true>(a, grid, nblk, lds, stream)
+               : launch_c64_codes<false, false>(a, grid, nblk, lds, stream);
 }
 
 }  // namespace tq

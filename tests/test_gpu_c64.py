@@ -133,3 +133,21 @@ def test_c64_ineligible_shapes_fall_back(monkeypatch):
     ref = _run(cv, lay_v, 9, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16)
     got = _run(cm, lay_m, 9, cfg=C64, sc=sc, sh=sh, res=res, kc_steps=lay_m.kc_steps)
     assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("batch", [64, 256])
+def test_c64_bench_size_default_grid(batch, monkeypatch):
+    """At the sizes the executor launches it (a 64- or 128-image chunk, the 256-image batch)
+    with the default grid -- one workgroup per CU, each walking its share of the 32-pixel
+    blocks (ranges of 24.5 / 98 blocks: partial last tiles) -- every form is the VALU
+    engine's bits."""
+    conv, x, sc, sh, res = _case(56, batch, seed=batch)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    for form in ("conv1", "conv2_out", "conv2_codes"):
+        kw = dict(FORMS[form])
+        if kw.pop("res", False):
+            kw["res"] = res
+        ref = _run(cv, lay_v, 56, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
+        got = _run(cm, lay_m, 56, cfg=C64, sc=sc, sh=sh, kc_steps=lay_m.kc_steps_nonneg, **kw)
+        for g, r in zip(got, ref):
+            assert (g is None and r is None) or torch.equal(g, r), form

@@ -38,6 +38,8 @@ from lstm_models import model as model_mod  # noqa: E402
 sys.path.insert(0, ROOT)
 from bench import HBM_PEAK_GBS, MFMA_F16_PEAK_TFLOPS, KernelTimer  # noqa: E402
 
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 vector = fp32 matrix peak
+
 
 def kernel_breakdown(fn, steps, total_s):
     """A second pass of `steps` steps with HIP events around every TQ kernel (tq_ops hook, as
@@ -120,6 +122,107 @@ def timed_graph(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
+class _Segments(object):
+    """HIP events around named segments of a forward on the current stream (a second,
+    instrumented pass: the events between kernels add a little idle time, so the shares are
+    of the instrumented step)."""
+
+    def __init__(self):
+        self.ev = []
+
+    def wrap(self, name, fn):
+        def run(*a, **k):
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = fn(*a, **k)
+            e1.record(s)
+            self.ev.append((name, e0, e1))
+            return r
+        return run
+
+    def totals(self):
+        out = {}
+        for name, e0, e1 in self.ev:
+            out[name] = out.get(name, 0.0) + e0.elapsed_time(e1) * 1e-3
+        return out
+
+
+def lstm_breakdown(qt, model, x, hidden, steps):
+    """Where the term-pair LSTM-650 chunk's time goes (BASELINE configs[2]): the instrumented
+    forward's kernel families -- the layer-0 input projection (TR(emb) encode + the term-pair
+    GEMM, tq_ops.tr_linear), the two recurrences in wavefront order (tq_lstm_seq2_f32: T + 1
+    launches of lstm_step2_kernel), the fp32 decoder (torch Linear, the reference's
+    TRLinearLayer semantics: the unquantized input) and log_softmax -- each with its share of
+    the instrumented step and its roofline."""
+    import tq_native
+    seg = _Segments()
+    saved = (tq_native.lstm_seq2, tq_ops.tr_linear, qt.decoder.forward)
+    tq_native.lstm_seq2 = seg.wrap("recurrence", saved[0])
+    tq_ops.tr_linear = seg.wrap("input_projection", saved[1])
+    qt.decoder.forward = seg.wrap("decoder", saved[2])
+    import torch.nn.functional as F
+    lsm = F.log_softmax
+    F.log_softmax = seg.wrap("log_softmax", lsm)
+    try:
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(steps):
+            qt(x, hidden)
+        e1.record(s)
+        torch.cuda.synchronize()
+    finally:
+        tq_native.lstm_seq2, tq_ops.tr_linear = saved[0], saved[1]
+        qt.decoder.forward = saved[2]
+        F.log_softmax = lsm
+    step = e0.elapsed_time(e1) * 1e-3 / steps
+    tot = {k: v / steps for k, v in seg.totals().items()}
+    T, B = x.shape
+    H, V = model.nhid, model.ntoken
+    D = model.encoder.embedding_dim
+    fam = {}
+    if "recurrence" in tot:
+        launches = T + 1
+        # bytes a launch must read: W_hh0, W_ih1, W_hh1 (fp32 [4H][H] each; launch s runs layer
+        # 0's step s and layer 1's step s - 1), 20.3 MB -- resident in the 256 MB MALL after the
+        # first step, so the HBM figure is a floor-of-floors
+        wbytes = 3 * 4 * H * H * 4
+        per = tot["recurrence"] / launches
+        fam["lstm_step2_kernel"] = {
+            "launches_per_step": launches, "avg_launch_us": per * 1e6,
+            "share_of_step": tot["recurrence"] / step, "bound": "hbm",
+            "bytes_per_launch": wbytes, "achieved_gbs": wbytes / per / 1e9,
+            "peak_gbs": HBM_PEAK_GBS, "frac": wbytes / per / 1e9 / HBM_PEAK_GBS}
+    if "input_projection" in tot:
+        prods = T * B * D * 4 * H
+        tf = 2 * prods / tot["input_projection"] / 1e12
+        fam["input_projection"] = {
+            "what": "TR(emb) codes + term-pair GEMM %dx%d -> %d (MFMA engine)" % (
+                T * B, D, 4 * H),
+            "avg_us": tot["input_projection"] * 1e6,
+            "share_of_step": tot["input_projection"] / step, "bound": "mfma",
+            "achieved_tflops": tf, "peak_tflops": MFMA_F16_PEAK_TFLOPS,
+            "frac": tf / MFMA_F16_PEAK_TFLOPS}
+    if "decoder" in tot:
+        tf = 2 * T * B * H * V / tot["decoder"] / 1e12
+        fam["decoder_fp32"] = {
+            "what": "torch fp32 Linear %d -> %d on %d rows (reference semantics)" % (H, V, T * B),
+            "avg_us": tot["decoder"] * 1e6, "share_of_step": tot["decoder"] / step,
+            "bound": "fp32", "achieved_tflops": tf, "peak_tflops": FP32_PEAK_TFLOPS,
+            "frac": tf / FP32_PEAK_TFLOPS}
+    if "log_softmax" in tot:
+        nb = 2 * T * B * V * 4
+        fam["log_softmax"] = {
+            "avg_us": tot["log_softmax"] * 1e6, "share_of_step": tot["log_softmax"] / step,
+            "bound": "hbm", "bytes": nb, "achieved_gbs": nb / tot["log_softmax"] / 1e9,
+            "peak_gbs": HBM_PEAK_GBS, "frac": nb / tot["log_softmax"] / 1e9 / HBM_PEAK_GBS}
+    rest = step - sum(tot.values())
+    fam["other"] = {"what": "embedding, h0/c0 TR, copies, launch gaps", "avg_us": rest * 1e6,
+                    "share_of_step": rest / step}
+    return {"instrumented_step_ms": step * 1e3, "families": fam}
+
+
 def lstm(args, dev):
     torch.manual_seed(1111)
     ntokens, bsz, bptt = evaluate_lstm.WT2_VOCAB, 10, 35
@@ -141,8 +244,11 @@ def lstm(args, dev):
         qt(x, model.init_hidden(bsz))
         tr_layer.set_tr_tracking(qt, False)
         t_tp = timed(lambda: qt(x, hidden), args.steps, args.warmup)
+        breakdown = lstm_breakdown(qt, model, x, hidden, args.steps)
         # the decoder as a term-pair GEMM (TRLinearLayer(quantize_input=True): linear(TR(h),
-        # TR(W)) on the MFMA engine), timed alone on the 350 x 650 LSTM output
+        # TR(W)) on the MFMA engine), timed alone on the 350 x 650 LSTM output -- not on the
+        # timed path (the reference's TRLinearLayer runs the dense layer on the unquantized
+        # input), reported as the secondary term-pair line
         dec = torch.nn.Linear(650, ntokens).to(dev)
         dec.weight.data.copy_(model.decoder.weight.data)
         dec.bias.data.copy_(model.decoder.bias.data)
@@ -161,6 +267,7 @@ def lstm(args, dev):
             "analytic_term_pair_macs_per_step": tmacs,
             "analytic_term_pair_macs_per_s": tmacs / t,
             "termpair_lstm_tokens_per_s": toks / t_tp,
+            "termpair_breakdown": breakdown,
             "term_pair_decoder": {
                 "what": "TRLinearLayer(quantize_input=True) 650 -> %d on %d rows, term-pair "
                         "GEMM on the MFMA engine, timed alone" % (ntokens, toks),
@@ -252,12 +359,18 @@ def d4_summary(dev, steps=10, warmup=3, batch=256):
     a = argparse.Namespace(steps=steps, warmup=warmup, batch=batch)
     out = {}
     r = lstm(a, dev)
+    fams = r["termpair_breakdown"]["families"]
+    dom = max((k for k in fams if k != "other"), key=lambda k: fams[k]["share_of_step"])
     out["lstm650"] = {"tokens_per_s": r["termpair_lstm_tokens_per_s"],
                       "tokens_per_s_miopen_composition": r["value"],
-                      "dominant_kernel": "term-pair decoder GEMM (650 -> 33278, 350 rows)",
-                      "roofline": dict(r["term_pair_decoder"], bound="mfma",
-                                       peak_tflops=MFMA_F16_PEAK_TFLOPS,
-                                       frac=r["term_pair_decoder"]["frac_of_fp16_mfma_peak"]),
+                      # the timed path's kernel families; roofline = the dominant one's
+                      "dominant_kernel": dom,
+                      "roofline": dict(fams[dom], kernel=dom),
+                      "families": fams,
+                      "term_pair_decoder_alone": dict(
+                          r["term_pair_decoder"], bound="mfma", peak_tflops=MFMA_F16_PEAK_TFLOPS,
+                          frac=r["term_pair_decoder"]["frac_of_fp16_mfma_peak"],
+                          on_timed_path=False),
                       "config": r["config"]}
     for arch in ("mobilenet_v2", "efficientnet_b0"):
         out[arch] = cnn_fused(arch, steps, warmup, batch, dev)
