@@ -40,6 +40,8 @@ import util  # noqa: E402
 
 METRIC = "term-pair MACs/sec + images/sec, ResNet-18 TQ g=8 at 1/2/4/8 MI355X"
 WB, G, K, DB, DT = 9, 8, 12, 9, 3
+STEM_NAMES = {"fused": "split-fp16 near-fp32 (fused stem kernel)",
+              "fp32": "torch fp32 conv (MIOpen) + BN/ReLU/max-pool/codes kernel"}
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 HBM_BYTES_PER_IMAGE = 15026432   # algorithmic bytes of the TR path per image
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes x clock = 78.6e12 lane-op/s
@@ -79,6 +81,11 @@ def parse(argv=None):
     ap.add_argument("--no-d4", action="store_true",
                     help="skip the d4 key (BASELINE configs[2]/[3]: LSTM-650, fused "
                          "MobileNet-V2 / EfficientNet-b0; rank 0 at N=1 only)")
+    ap.add_argument("--stem", choices=("fused", "fp32"), default="fused",
+                    help="fused: the stem conv in the fused stem kernel (split-fp16 near-fp32); "
+                         "fp32: torch's fp32 conv + the BN/ReLU/max-pool/codes kernel")
+    ap.add_argument("--no-stem-leg", action="store_true",
+                    help="skip the second timed pass with the other stem (N=1 only)")
     ap.add_argument("--unfused", action="store_true",
                     help="run the module path (separate BN/ReLU/add/TR passes) instead of "
                          "the fused executor")
@@ -420,7 +427,7 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=dev)
 
     model_fp, qmodel, tmacs_per_img = build_model(dev, args.batch, rank)
-    runner = qmodel if args.unfused else tq_fuse.FusedResNet(qmodel)
+    runner = qmodel if args.unfused else tq_fuse.FusedResNet(qmodel, stem=args.stem)
 
     # resident synthetic inputs (two batches, alternated) and labels
     data = util.SyntheticImageNet(2 * args.batch, args.batch, seed=rank, device=dev)
@@ -435,13 +442,15 @@ def main(argv=None):
     if args.streams > 1 and not args.unfused:
         streams = [torch.cuda.Stream(dev) for _ in range(args.streams)]
 
-    def step(i):
-        x, y = batches[i % 2]
-        out = runner(x) if streams is None else runner.forward_streams(x, streams)
-        counters[0] += (out.argmax(1) == y).sum()
-        counters[1] += y.numel()
+    def timed_steps(runner):
+        """W untimed warmup steps, (optionally) one hipGraph per resident batch, then the K
+        timed steps between barrier + synchronize: (seconds, launch mode, counters)."""
+        def step(i):
+            x, y = batches[i % 2]
+            out = runner(x) if streams is None else runner.forward_streams(x, streams)
+            counters[0] += (out.argmax(1) == y).sum()
+            counters[1] += y.numel()
 
-    with torch.no_grad():
         for i in range(args.warmup):
             step(i)
         torch.cuda.synchronize()
@@ -482,8 +491,10 @@ def main(argv=None):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        elapsed = time.perf_counter() - t0
-        acc_counters = [int(v) for v in counters.tolist()]
+        return time.perf_counter() - t0, launch, [int(v) for v in counters.tolist()]
+
+    with torch.no_grad():
+        elapsed, launch, acc_counters = timed_steps(runner)
 
         # Kernel roofline pass: the same K steps again, eager, with HIP events around every
         # TQ kernel on its launch stream (events between kernels cost ~10 us of idle GPU
@@ -501,6 +512,17 @@ def main(argv=None):
         tq_ops.set_kernel_hook(None)
         # GPU time of that one-stream pass (its kernels plus the event gaps between them)
         roof_pass_s = timer.base.elapsed_time(pass_end) * 1e-3
+
+        # the other stem: the same executor with the torch fp32 stem conv
+        # (MIOpen, true fp32) + the BN/ReLU/max-pool/codes kernel, timed the same way -- the
+        # price of the fused split-fp16 stem's precision choice, reported beside the headline
+        stem_leg = None
+        if world == 1 and not args.unfused and not args.no_stem_leg:
+            other = "fp32" if args.stem == "fused" else "fused"
+            el2, launch2, _ = timed_steps(tq_fuse.FusedResNet(qmodel, stem=other))
+            stem_leg = {"stem": STEM_NAMES[other], "images_per_s": args.batch * args.steps / el2,
+                        "ms_per_step": el2 / args.steps * 1e3, "launch": launch2,
+                        "streams": args.streams}
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -652,15 +674,17 @@ def main(argv=None):
                                    "epilogue)",
                        "launch": launch, "streams": args.streams,
                        # the stem conv (not a TR layer; fp32 torch in the reference) runs in
-                       # the fused stem kernel as a split-fp16 near-fp32 conv
-                       "stem": "split-fp16 near-fp32 (fused stem kernel)"
-                               if enc_name == "stem_conv_pool" else "torch fp32 conv"},
+                       # the fused stem kernel as a split-fp16 near-fp32 conv,
+                       # or (--stem fp32) as torch's fp32 conv
+                       "stem": STEM_NAMES["fused" if enc_name == "stem_conv_pool" else "fp32"]},
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,
             "roofline": roof,
             "roofline_tr": roof_tr,
             "accuracy_counters": acc_counters,
         }
+        if stem_leg is not None:
+            result["stem_fp32" if args.stem == "fused" else "stem_fused"] = stem_leg
         if world == 1 and not args.no_d1:
             result["d1_tr_op"] = d1_tr_op(dev)
         if world == 1 and not args.no_d4:

@@ -180,10 +180,17 @@ def _pool_params(mp):
 
 
 class FusedResNet(nn.Module):
-    """Inference executor over a converted + calibrated torchvision-style ResNet."""
+    """Inference executor over a converted + calibrated torchvision-style ResNet.
 
-    def __init__(self, qmodel):
+    ``stem="fused"`` (default) runs conv1 + bn1 + relu + maxpool + the first codes as one
+    kernel whose conv is split-fp16 near-fp32; ``stem="fp32"`` keeps torch's fp32
+    conv1 (MIOpen's true fp32: gfx950 has no TF32 / xf32) and runs only BN + ReLU + max-pool +
+    codes in one kernel -- the reference's arithmetic for the stem conv (bench.py --stem)."""
+
+    def __init__(self, qmodel, stem="fused"):
         super(FusedResNet, self).__init__()
+        if stem not in ("fused", "fp32"):
+            raise ValueError("stem must be 'fused' or 'fp32'")
         self.qmodel = qmodel
         self.blocks = []
         for layer in (qmodel.layer1, qmodel.layer2, qmodel.layer3, qmodel.layer4):
@@ -202,7 +209,8 @@ class FusedResNet(nn.Module):
         # torchvision shape: conv 7x7/2 pad 3, 3 -> 64, no bias; pool 3x3/2 pad 1
         c1 = qmodel.conv1
         self.stem_w = None
-        if (self.fuse_stem and self.pool == (3, 2, 1) and isinstance(c1, nn.Conv2d)
+        if (stem == "fused" and self.fuse_stem and self.pool == (3, 2, 1) and
+                isinstance(c1, nn.Conv2d)
                 and type(c1) is nn.Conv2d and c1.in_channels == 3 and c1.out_channels == 64
                 and c1.kernel_size == (7, 7) and c1.stride == (2, 2) and c1.padding == (3, 3)
                 and c1.dilation == (1, 1) and c1.groups == 1 and c1.bias is None

@@ -95,6 +95,46 @@ def _check_stem(q, x, rec, module_stem):
 
 def test_fused_efficientnet_b0_teacher_forced(net):
     q, x = net
+    _teacher_forced(q, x, SAMPLE)
+
+
+def _bench_batch(seed=1):
+    torch.manual_seed(seed)
+    return torch.randn(256, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+
+
+def test_fused_efficientnet_b0_teacher_forced_at_bench_size(net):
+    """The same layer-by-layer check on the batch the bench times (256 images: the SE gate
+    kernel's 256 workgroups, the gate-and-encode pass's fixed-chunk index path, the expand
+    engine's persistent grid, the depthwise segment walks), on images at both ends of both
+    128-image chunks."""
+    q, _ = net
+    _teacher_forced(q, _bench_batch(), [0, 127, 128, 255])
+
+
+def test_fused_efficientnet_b0_bench_size_variants_bit_identical(net, monkeypatch):
+    """At 256 images: the bench's two 128-image chunk streams, and the default dispatch against
+    the expand engine off (TQ_XP=0), the module-call squeeze-excite (TQ_SE_FUSED=0), the
+    gate-and-encode pass's division form (TQ_AEA_FIXED=0) and the generic epilogues
+    (TQ_EPI_FAST=0, TQ_DW_FAST=0) -- the same logits bit for bit."""
+    q, _ = net
+    x = _bench_batch()
+    fused = tq_fuse.FusedEfficientNet(q)
+    with torch.no_grad():
+        ref = fused(x).view(torch.int32)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        assert torch.equal(fused.forward_streams(x, streams).view(torch.int32), ref)
+        for env in ({"TQ_XP": "0"}, {"TQ_SE_FUSED": "0"}, {"TQ_AEA_FIXED": "0"},
+                    {"TQ_EPI_FAST": "0", "TQ_DW_FAST": "0"}):
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            assert torch.equal(fused(x).view(torch.int32), ref), env
+            for k in env:
+                monkeypatch.delenv(k)
+    torch.cuda.synchronize()
+
+
+def _teacher_forced(q, x, sample):
     fused = tq_fuse.FusedEfficientNet(q)
     cap = []
     logits_cap = fused(x, capture=cap)
@@ -109,8 +149,8 @@ def test_fused_efficientnet_b0_teacher_forced(net):
         sf = (conv.consumer.quant if rec["kind"] == "dw" else conv.quant)[0]
         c = layer.conv
         c_in = c.in_channels
-        assert bool((rec["codes_in"][SAMPLE][..., c_in:] == 0).all()), rec["name"]
-        xq = _codes(rec["codes_in"], SAMPLE, c_in) * float(np.float32(sf))
+        assert bool((rec["codes_in"][sample][..., c_in:] == 0).all()), rec["name"]
+        xq = _codes(rec["codes_in"], sample, c_in) * float(np.float32(sf))
         top, bottom, left, right = tq_ops.static_padding(c)
         xq = F.pad(xq, (left, right, top, bottom))
         wq = c.weight.detach().double().cpu()
@@ -119,18 +159,18 @@ def test_fused_efficientnet_b0_teacher_forced(net):
         ref, a = _bn(conv.bn, z)
         bound_mag = mag * a.abs().view(1, -1, 1, 1)
         if rec["residual"] is not None:
-            r = _nchw(rec["residual"], SAMPLE)
+            r = _nchw(rec["residual"], sample)
             ref = ref + r
             bound_mag = bound_mag + r.abs()
         bound = 1e-5 * torch.maximum(ref.abs(), bound_mag)
         if rec["act"] == "swish":
             ref = ref * torch.sigmoid(ref)
             bound = 1.1 * bound + 1e-6 * ref.abs()
-        y = _nchw(rec["out"], SAMPLE)
+        y = _nchw(rec["out"], sample)
         err = (y - ref).abs()
         assert bool((err <= bound + 1e-30).all()), (rec["name"], float((err / bound).max()))
         if rec.get("post") is not None:  # the swish pass after an expand conv's BN output
-            post = _nchw(rec["post"], SAMPLE)
+            post = _nchw(rec["post"], sample)
             sw = y * torch.sigmoid(y)
             assert bool(((post - sw).abs() <= 1e-6 * sw.abs() + 1e-7 * y.abs() + 1e-30).all()), \
                 rec["name"]
@@ -142,9 +182,9 @@ def test_fused_efficientnet_b0_teacher_forced(net):
         co = y.shape[1]
         val = y
         if rec.get("gate") is not None:  # fp32(gate * y), as the module's sigmoid(x_sq) * x
-            g = rec["gate"][SAMPLE].cpu().float().view(len(SAMPLE), co, 1, 1)
+            g = rec["gate"][sample].cpu().float().view(len(sample), co, 1, 1)
             val = (g * y.float()).double()
-        got = _codes(rec["codes_out"], SAMPLE, co).long()
+        got = _codes(rec["codes_out"], sample, co).long()
         assert torch.equal(got, _tr_codes(val, quant)), rec["name"]
 
 

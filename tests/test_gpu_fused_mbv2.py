@@ -75,6 +75,44 @@ def _check_stem(q, x, rec, module_stem):
 
 def test_fused_mobilenet_v2_teacher_forced(net):
     q, x = net
+    _teacher_forced(q, x, SAMPLE)
+
+
+def _bench_batch(seed=1):
+    torch.manual_seed(seed)
+    return torch.randn(256, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+
+
+def test_fused_mobilenet_v2_teacher_forced_at_bench_size(net):
+    """The same layer-by-layer check on the batch the bench times (256 images: the expand
+    engine's persistent grid, the depthwise kernel's segment walks and the large-N index math
+    of every kernel at the timed size), on images at both ends of both 128-image chunks."""
+    q, _ = net
+    _teacher_forced(q, _bench_batch(), [0, 127, 128, 255])
+
+
+def test_fused_mobilenet_v2_bench_size_variants_bit_identical(net, monkeypatch):
+    """At 256 images: the bench's two 128-image chunk streams, and the default dispatch against
+    the expand engine off (TQ_XP=0) and the generic epilogues (TQ_EPI_FAST=0, TQ_DW_FAST=0) --
+    the same logits bit for bit (so the chunked launches the bench times inherit the 256-image
+    teacher-forced parity above)."""
+    q, _ = net
+    x = _bench_batch()
+    fused = tq_fuse.FusedMobileNetV2(q)
+    with torch.no_grad():
+        ref = fused(x).view(torch.int32)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        assert torch.equal(fused.forward_streams(x, streams).view(torch.int32), ref)
+        for env in ({"TQ_XP": "0"}, {"TQ_EPI_FAST": "0", "TQ_DW_FAST": "0"}):
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            assert torch.equal(fused(x).view(torch.int32), ref), env
+            for k in env:
+                monkeypatch.delenv(k)
+    torch.cuda.synchronize()
+
+
+def _teacher_forced(q, x, sample):
     fused = tq_fuse.FusedMobileNetV2(q)
     cap = []
     logits_cap = fused(x, capture=cap)
@@ -87,11 +125,11 @@ def test_fused_mobilenet_v2_teacher_forced(net):
         layer = conv.layer
         sf, db, dt = conv.consumer.quant if rec["kind"] == "dw" else conv.quant
         c_in = layer.conv.in_channels
-        codes = _codes(rec["codes_in"], SAMPLE, c_in)
+        codes = _codes(rec["codes_in"], sample, c_in)
         # (i) input codes are exact TR codes: v * sf reproduces TR of some fp32 value and every
         # code is a kept-term value of its own quantized magnitude (checked through the
         # producer below: codes_out == TR(out))
-        assert bool((rec["codes_in"][SAMPLE][..., c_in:] == 0).all()), rec["name"]
+        assert bool((rec["codes_in"][sample][..., c_in:] == 0).all()), rec["name"]
         xq = codes * float(np.float32(sf))
         wq = layer.conv.weight.detach().double().cpu()
         c = layer.conv
@@ -101,12 +139,12 @@ def test_fused_mobilenet_v2_teacher_forced(net):
         ref, a = _bn(conv.bn, z)
         bound_mag = mag * a.abs().view(1, -1, 1, 1)
         if rec["residual"] is not None:
-            r = _nchw(rec["residual"], SAMPLE)
+            r = _nchw(rec["residual"], sample)
             ref = ref + r
             bound_mag = bound_mag + r.abs()
         if rec["relu"] == 6:
             ref = ref.clamp(0, 6)
-        y = _nchw(rec["out"], SAMPLE)
+        y = _nchw(rec["out"], sample)
         err = (y - ref).abs()
         bound = 1e-5 * torch.maximum(ref.abs(), bound_mag) + 1e-30
         assert bool((err <= bound).all()), (rec["name"], float((err / bound).max()))
@@ -122,7 +160,7 @@ def test_fused_mobilenet_v2_teacher_forced(net):
             co = y.shape[1]
             yq = oracle.tr(y.float().numpy().reshape(1, -1, 1, 1), sf2, db2, 1, dt2)
             exp = np.rint(yq.reshape(y.shape) / np.float32(sf2)).astype(np.int64)
-            got = _codes(rec["codes_out"], SAMPLE, co).long()
+            got = _codes(rec["codes_out"], sample, co).long()
             assert torch.equal(got, torch.from_numpy(exp)), rec["name"]
 
 

@@ -232,7 +232,8 @@ def test_free_running_drift_from_module_path(bench_model):
     path (TRConv2dLayer + torch BN / ReLU / add: the reference composition) on the whole
     256-image bench batch, with nothing teacher forced -- so the midpoint code flips of the
     stem and BN-fold seams propagate through all 19 layers.  Records the top-1 agreement and
-    the logit deviation max |dlogit| / max |logit|."""
+    the logit deviation max |dlogit| / max |logit| (measured 1.0000 and
+    4.9e-3, bounded at about twice that)."""
     qmodel, x = bench_model
     fused = tq_fuse.FusedResNet(qmodel)
     with torch.no_grad():
@@ -244,7 +245,7 @@ def test_free_running_drift_from_module_path(bench_model):
     mean_dev = float((lf - lm).abs().mean() / lm.abs().mean())
     print("free-running drift (256 images): top-1 agreement %.4f, max |dlogit| / max |logit| "
           "%.3e, mean |dlogit| / mean |logit| %.3e" % (agree, dev, mean_dev))
-    assert agree >= 0.95 and dev <= 5e-2, (agree, dev)
+    assert agree >= 0.99 and dev <= 1e-2, (agree, dev)
 
 
 def fused_next(rec, r):
@@ -347,3 +348,69 @@ def test_fused_stem_codes_vs_miopen_fp32_stem(bench_model):
     print("stem seam: %d of %d layer1.0 input codes differ from TR of the MIOpen fp32 stem "
           "(%.2e)" % (flips, total, flips / total))
     assert flips <= total * 1e-4, (flips, total)
+
+
+def _tr_ints(y, quant):
+    """oracle.tr integer term sums of an NHWC fp32 array (threaded over 8 chunks)."""
+    from concurrent.futures import ThreadPoolExecutor
+    sf, db, dt = quant
+    flat = y.reshape(-1)
+    out = np.empty_like(flat)
+    bounds = np.linspace(0, flat.size, 17).astype(np.int64)
+
+    def run(j):
+        lo, hi = bounds[j], bounds[j + 1]
+        out[lo:hi] = oracle.tr(flat[lo:hi].reshape(1, -1, 1, 1), sf, db, 1, dt).reshape(-1)
+    with ThreadPoolExecutor(8) as ex:
+        list(ex.map(run, range(16)))
+    return np.rint(out.astype(np.float64) / float(np.float32(sf))).astype(np.int64).reshape(
+        y.shape)
+
+
+def test_stem_seam_within_the_fp32_spread(bench_model):
+    """Is the fused split-fp16 stem's flip rate inside the spread of two fp32 stems?  On 48
+    bench images: layer1.0's input codes as TR of (a) MIOpen's fp32 conv1 -> bn1 -> relu ->
+    maxpool (the module path on the GPU), (b) the same composition in fp32 on the CPU (another
+    summation order, as the reference's own cuDNN conv had), (c) the fused stem kernel, and
+    (d) the executor's --stem fp32 leg (MIOpen conv + the BN/ReLU/max-pool/codes kernel).
+    Every pair's flips must be one-step midpoint straddles; the fused stem may flip at most
+    4x as many codes against either fp32 stem as the two fp32 stems flip between themselves
+    (floor: 1e-5 of the codes).  Prints the counts."""
+    qmodel, x = bench_model
+    x = x[:48].contiguous(memory_format=torch.channels_last)
+    m = qmodel
+    with torch.no_grad():
+        rec = []
+        tq_fuse.FusedResNet(qmodel)(x, capture=rec)
+        rec32 = []
+        tq_fuse.FusedResNet(qmodel, stem="fp32")(x, capture=rec32)
+        ya = m.maxpool(m.relu(m.bn1(m.conv1(x))))
+        import copy
+        c1, b1 = copy.deepcopy(m.conv1).cpu(), copy.deepcopy(m.bn1).cpu()
+        yb = m.maxpool(m.relu(b1(c1(x.cpu().contiguous()))))
+    quant = rec[1]["conv"].quant
+    nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().cpu().numpy()  # noqa: E731
+    ya, yb = nhwc(ya), nhwc(yb)
+    qa, qb = _tr_ints(ya, quant), _tr_ints(yb, quant)
+    qc = rec[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
+    qd = rec32[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
+    vals = {"a": ya, "b": yb, "c": nhwc(rec[0]["out"]), "d": nhwc(rec32[0]["out"])}
+    codes = {"a": qa, "b": qb, "c": qc, "d": qd}
+    flips = {}
+    for p, q in (("a", "b"), ("c", "a"), ("c", "b"), ("d", "a"), ("d", "b"), ("c", "d")):
+        mism = codes[p] != codes[q]
+        flips[p + q] = int(mism.sum())
+        if flips[p + q]:
+            qp, qq = _quantize(vals[p][mism], quant), _quantize(vals[q][mism], quant)
+            assert np.all(np.abs(qp - qq) == 1), p + q
+            mid = np.minimum(qp, qq).astype(np.float64) + 0.5
+            s32 = np.float32(quant[0])
+            rp = (np.abs(vals[p][mism]) / s32).astype(np.float32).astype(np.float64)
+            rq = (np.abs(vals[q][mism]) / s32).astype(np.float32).astype(np.float64)
+            assert np.all((np.minimum(rp, rq) <= mid) & (mid <= np.maximum(rp, rq))), p + q
+    total = qa.size
+    print("stem fp32 spread (48 images, %d codes): MIOpen vs CPU fp32 %d; fused split-fp16 vs "
+          "MIOpen %d, vs CPU %d; --stem fp32 leg vs MIOpen %d, vs CPU %d; fused vs fp32 leg %d"
+          % (total, flips["ab"], flips["ca"], flips["cb"], flips["da"], flips["db"], flips["cd"]))
+    bound = max(4 * flips["ab"], int(total * 1e-5))
+    assert flips["ca"] <= bound and flips["cb"] <= bound, flips
