@@ -48,6 +48,16 @@
 #include "tq_device.h"
 #include "tq_launch.h"
 
+#ifndef STEM_AB
+#define STEM_AB 0  // timing-only ablation builds (tools/variant1.sh); 0 = the product kernel
+#endif
+#ifndef STEM_CARRY
+#define STEM_CARRY 1  // 1: a tile's first conv row carried from the tile above (one strip per wave)
+#endif
+#ifndef STEM_PF
+#define STEM_PF 0  // 1: the next K-step's input slices read during this step's MFMAs
+#endif
+
 namespace tq {
 
 namespace {
@@ -72,7 +82,9 @@ __device__ __forceinline__ float row_down(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(b, b, 0x100 + D, 0xf, 0xf, false));
 }
 
-template <int TP, int QMAX>
+// ONE: one strip per wave (nb <= 8 waves: Wo <= 56), the strip's last conv row carried to
+// the next tile (STEM_CARRY)
+template <int TP, int QMAX, bool ONE>
 __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArgs a, int sc,
                                                                          int nb, int tiles) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds_raw[];
@@ -196,6 +208,10 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   // (it & 1) is written before barrier A and read between A and B, the other slot is
   // cleared between A and B for the next tile.
   int it = 0;
+  // one strip per wave (Wo <= 56): each wave keeps its strip's last conv row for the next tile
+  constexpr bool one = ONE;
+  f32x4 carry[4];
+  int prev_tile = -2, prev_kx = 0;
   for (int tile = t_begin; tile < t_end; ++tile, ++it) {
     const int n = tile / tpi;
     const int py0 = (tile - n * tpi) * TP;
@@ -223,12 +239,12 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       kx = kStemXMag - e;
     }
     const int kback = -(kx + kStemWExp);
-    commit(kx);
+    if (STEM_AB != 3) commit(kx);  // (3: timing only, no input staging)
     if (tid == 0) tile_max[(it + 1) & 1] = 0u;
     __syncthreads();  // B
-    if (tile + 1 < t_end) prefetch(tile + 1);
+    if (STEM_AB != 3 && tile + 1 < t_end) prefetch(tile + 1);
 
-    for (int b = wave; b < nb; b += kStemThreads / 64) {
+    for (int b = wave; b < nb; b += ONE ? nb : kStemThreads / 64) {
       const int c0 = 14 * b - 1;  // first conv column of the strip
       const int ox = c0 + i16;
       const bool colok = ox >= 0 && ox < Wc;
@@ -258,14 +274,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         for (int r = 0; r < NR; ++r)
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) acc[r][mb] = (f32x4)0.0f;
-#pragma unroll 1
-        for (int ks = 0; ks < kStemK / 32; ++ks) {
-          // (no register double buffer of the input slices: with four rows in flight their
-          // loads' latency hides behind the other rows' MFMAs, and the registers are full)
-          f16x8 x0[NR], x1[NR];
-#pragma unroll
-          for (int r = 0; r < NR; ++r) load_x(rr + r, ks, x0[r], x1[r]);
-          {
+        auto mfmas = [&](int ks, const f16x8 (&x0)[NR], const f16x8 (&x1)[NR])
+            __attribute__((always_inline)) {
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) {
             const uint16_t* wr = ws + (mb * 16 + i16) * kStemWRow + 32 * ks + 8 * g;
@@ -274,14 +284,45 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
               f32x4 c = acc[r][mb];
+#if STEM_AB == 2  // timing only: no MFMA
+              asm volatile("" : "+v"(c) : "v"(w0), "v"(w1), "v"(x0[r]), "v"(x1[r]));
+#else
               c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, x0[r], c, 0, 0, 0);
               c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, x1[r], c, 0, 0, 0);
               c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, x0[r], c, 0, 0, 0);
+#endif
               acc[r][mb] = c;
             }
           }
+        };
+#if STEM_PF
+        // the next K-step's input slices are read before this step's MFMAs (two register
+        // buffers, the K loop unrolled so both stay in registers)
+        f16x8 xa0[NR], xa1[NR], xb0[NR], xb1[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) load_x(rr + r, 0, xa0[r], xa1[r]);
+#pragma unroll
+        for (int ks = 0; ks < kStemK / 32; ks += 2) {
+#pragma unroll
+          for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 1, xb0[r], xb1[r]);
+          mfmas(ks, xa0, xa1);
+          if (ks + 2 < kStemK / 32) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) load_x(rr + r, ks + 2, xa0[r], xa1[r]);
           }
+          mfmas(ks + 1, xb0, xb1);
         }
+#else
+#pragma unroll 1
+        for (int ks = 0; ks < kStemK / 32; ++ks) {
+          // (no register double buffer of the input slices: with four rows in flight their
+          // loads' latency hides behind the other rows' MFMAs, and the registers are full)
+          f16x8 x0[NR], x1[NR];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) load_x(rr + r, ks, x0[r], x1[r]);
+          mfmas(ks, x0, x1);
+        }
+#endif
         // raw (sign-adjusted) sums; conv positions outside the image pool as -inf
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -298,6 +339,10 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       // (2i, 2i+1); row 2i closes pool row i-1 and, with row 2i+1, opens pool row i.
       auto emit_pool = [&](int j, const f32x4 (&run)[4], const f32x4 (&last)[4]) {
         const int py = py0 + j;
+        if (STEM_AB == 1) {  // timing only: no pool / BN / stores (values kept live)
+          asm volatile("" ::"v"(run[0]), "v"(last[3]));
+          return;
+        }
         float m[4][4];
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
@@ -375,6 +420,36 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       // row TP-1.
       f32x4 run[4];
       f32x4 y[4][4];
+      if constexpr (STEM_CARRY && one) {
+        // conv row 2 py0 - 1 (rr = 0) is the previous tile's last one (rr = 2 TP) when this
+        // wave's previous tile was the one above in the same image (a workgroup walks its
+        // tiles top to bottom) and scaled its inputs by the same 2^kx (the raw sums are in
+        // the tile's scale; equal scales give the same fp16 splits, so the carried sums are
+        // bit for bit the ones this tile would compute), -inf above the image, else computed:
+        // 2 TP conv rows per tile instead of 2 TP + 1
+        if (py0 == 0) {
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) carry[mb] = (f32x4)(-__builtin_inff());
+        } else if (!(tile == prev_tile + 1 && n == prev_tile / tpi && kx == prev_kx)) {
+          conv_rows(std::integral_constant<int, 1>(), 0, y);
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) carry[mb] = y[0][mb];
+        }
+#pragma unroll 1
+        for (int p = 0; p < TP / 2; ++p) {
+          conv_rows(std::integral_constant<int, 4>(), 4 * p + 1, y);
+          // pool row 2p: rr 4p (carry), 4p + 1, 4p + 2; pool row 2p + 1: rr 4p + 2 .. 4p + 4
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(carry[mb], y[0][mb]);
+          emit_pool(2 * p, run, y[1]);
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[1][mb], y[2][mb]);
+          emit_pool(2 * p + 1, run, y[3]);
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) carry[mb] = y[3][mb];
+        }
+        continue;
+      } else {
 #pragma unroll 1
       for (int p = 0; p < TP / 2; ++p) {
         conv_rows(std::integral_constant<int, 4>(), 4 * p, y);
@@ -387,12 +462,15 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       }
       conv_rows(std::integral_constant<int, 1>(), 2 * TP, y);
       emit_pool(TP - 1, run, y[0]);
+      }
     }
+    prev_tile = tile;
+    prev_kx = kx;
   }
 }
 
-template <int TP, int QMAX>
-hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
+template <int TP, int QMAX, bool ONE>
+hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
   const int nb = (a.Wo + 6) / 7;
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
   int64_t bytes =
@@ -407,7 +485,7 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   }
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP, QMAX>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP, QMAX, ONE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kStemDynLds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -419,9 +497,16 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
     cus = 256;
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return hipSuccess;
-  stem_conv_pool_kernel<TP, QMAX><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(
+  stem_conv_pool_kernel<TP, QMAX, ONE><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(
       b, sc, nb, tiles);
   return hipGetLastError();
+}
+
+template <int TP, int QMAX>
+hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
+  const int nb = (a.Wo + 6) / 7;
+  return nb <= kStemThreads / 64 ? launch_stem_one<TP, QMAX, true>(a, stream)
+                                 : launch_stem_one<TP, QMAX, false>(a, stream);
 }
 
 }  // namespace

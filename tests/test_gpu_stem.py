@@ -71,3 +71,39 @@ def test_stem_rejects_bad_shapes():
     sc = torch.ones(64, device=DEV)
     with pytest.raises(RuntimeError, match="H, W % 4"):
         tq_native.stem_conv_pool_encode(x, wsplit, sc, sc, out)
+
+
+def test_stem_row_carry_is_bit_identical_to_separate_tiles():
+    """One strip per wave (Wo <= 56): a workgroup walking several tiles down an image carries
+    each tile's last conv row into the next tile instead of recomputing it -- only when both
+    tiles scaled their inputs by the same power of two.  40 images (560 tiles: runs of 2-3
+    tiles per workgroup, starting mid-image) with bands of rows scaled by 1e-3 / 40 (adjacent
+    tiles with different scales) give the same bits as every image launched alone (14 tiles
+    on 14 workgroups: no carry at all)."""
+    torch.manual_seed(7)
+    n = 40
+    x = torch.randn(n, 3, 224, 224)
+    x[:, :, 40:72] *= 1e-3    # tiles whose max |x| falls several binades
+    x[:, :, 150:160] *= 40.0  # and one that rises
+    x[1::3] *= 0.3
+    x = x.contiguous(memory_format=torch.channels_last).to(DEV)
+    wt = torch.empty(64, 3, 7, 7)
+    nn.init.kaiming_normal_(wt, mode="fan_out", nonlinearity="relu")
+    sc, sh = _bn_coefs(11)
+    sc, sh = sc.to(DEV), sh.to(DEV)
+    wsplit = tq_ops.pack_stem_weight(wt.to(DEV))
+
+    def run(xb):
+        out = torch.empty((xb.shape[0], 64, 56, 56), device=DEV).contiguous(
+            memory_format=torch.channels_last)
+        codes = torch.empty((xb.shape[0], 56, 56, 64), dtype=torch.float16, device=DEV)
+        tq_native.stem_conv_pool_encode(xb, wsplit, sc, sh, out, codes_a=codes,
+                                        quant_a=(0.05, 9, 3))
+        return out, codes
+
+    out, codes = run(x)
+    for i in (0, 1, 2, 17, 39):
+        o1, c1 = run(x[i:i + 1].contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+        assert torch.equal(out[i].view(torch.int32), o1[0].view(torch.int32)), i
+        assert torch.equal(codes[i].view(torch.int16), c1[0].view(torch.int16)), i
