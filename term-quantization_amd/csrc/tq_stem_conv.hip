@@ -339,8 +339,13 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       // (2i, 2i+1); row 2i closes pool row i-1 and, with row 2i+1, opens pool row i.
       auto emit_pool = [&](int j, const f32x4 (&run)[4], const f32x4 (&last)[4]) {
         const int py = py0 + j;
-        if (STEM_AB == 1) {  // timing only: no pool / BN / stores (values kept live)
-          asm volatile("" ::"v"(run[0]), "v"(last[3]));
+        if (STEM_AB == 1) {  // timing only: no pool / BN / stores (every conv sum kept live)
+          float keep = 0.0f;
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) keep += run[mb][i] + last[mb][i];
+          asm volatile("" ::"v"(keep));
           return;
         }
         float m[4][4];
@@ -381,8 +386,12 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           float yv[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) yv[i] = fmaxf(fmaf(ldexpf(v4[i], kback), bsc[i], bsh[i]), 0.0f);
-          *reinterpret_cast<float4*>(a.out + p * 64 + co) =
-              make_float4(yv[0], yv[1], yv[2], yv[3]);
+          if (STEM_AB == 4) {  // timing only: no stores (values kept live)
+            asm volatile("" ::"v"(yv[0]), "v"(yv[1]), "v"(yv[2]), "v"(yv[3]));
+          } else {
+            *reinterpret_cast<float4*>(a.out + p * 64 + co) =
+                make_float4(yv[0], yv[1], yv[2], yv[3]);
+          }
 #pragma unroll
           for (int side = 0; side < 2; ++side) {
             int16_t* codes = side ? a.codes_b : a.codes_a;
@@ -407,8 +416,12 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
               for (int i = 0; i < 4; ++i)
                 v[i] = code_bits(tr_value_g1_inv(yv[i], inv, maxv, k), fmt);
             }
-            *reinterpret_cast<int2*>(codes + p * cp + co) =
-                make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+            if (STEM_AB == 4) {
+              asm volatile("" ::"v"(v[0] | (v[1] << 16)), "v"(v[2] | (v[3] << 16)));
+            } else {
+              *reinterpret_cast<int2*>(codes + p * cp + co) =
+                  make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+            }
           }
         }
         __builtin_amdgcn_wave_barrier();  // pb is rewritten by the next pool row

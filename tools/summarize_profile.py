@@ -23,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {  # summary key -> kernel-name substrings (every MFMA term-pair conv engine)
     "conv2d_tp": ("conv2d_tp_kernel",),
     "conv2d_tp_mfma": ("conv2d_tp_mfma", "conv2d_tp_patch", "conv2d_tp_direct",
-                       "conv2d_tp_strip", "conv2d_tp_ring", "conv2d_tp_pw"),
+                       "conv2d_tp_strip", "conv2d_tp_ring", "conv2d_tp_pw", "conv2d_tp_c64",
+                       "conv2d_tp_xp"),
     "act_encode": ("act_encode_kernel",),
     "stem_pool_encode": ("bn_relu_maxpool_encode_kernel",),
     "stem_conv_pool": ("stem_conv_pool_kernel",),
