@@ -278,6 +278,37 @@ def lstm(args, dev):
                        "batch": bsz, "bptt": bptt, "data": "synthetic token ids"}}
 
 
+def lstm_trace(chunks, dev):
+    """Profiling mode (tools/gpu_lstm_trace.sh): the term-pair LSTM-650 model of lstm() alone,
+    calibrated and warmed, then `chunks` 350-token forwards between synchronize calls; prints
+    the host clocks around them so tools/trace_window.py can cut exactly those chunks out of a
+    rocprofv3 kernel trace."""
+    torch.manual_seed(1111)
+    ntokens, bsz, bptt = evaluate_lstm.WT2_VOCAB, 10, 35
+    model = model_mod.RNNModel("LSTM", ntokens, 650, 650, 2, 0.5, True).to(dev).eval()
+    tr_params = evaluate_lstm.static_lstm_layer_settings(model, 8, 8, 12)
+    tokens = torch.randint(0, ntokens, (bptt * bsz * 4 + bsz,))
+    x = evaluate_lstm.get_batch(evaluate_lstm.batchify(tokens, bsz, dev), 0, bptt)[0]
+    with torch.no_grad():
+        qt = evaluate_lstm.convert_model(model, tr_params, 8, 8, termpair=True)
+        hidden = model.init_hidden(bsz)
+        qt(x, hidden)  # calibration pass
+        tr_layer.set_tr_tracking(qt, False)
+        for _ in range(3):
+            qt(x, hidden)
+        torch.cuda.synchronize()
+        clocks = {"monotonic": time.CLOCK_MONOTONIC, "boottime": time.CLOCK_BOOTTIME}
+        w0 = {k: time.clock_gettime_ns(c) for k, c in clocks.items()}
+        t0 = time.perf_counter()
+        for _ in range(chunks):
+            qt(x, hidden)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / chunks
+        w1 = {k: time.clock_gettime_ns(c) for k, c in clocks.items()}
+    return {"chunks": chunks, "tokens_per_chunk": bptt * bsz, "ms_per_chunk": t * 1e3,
+            "tokens_per_s": bptt * bsz / t, "window_ns": {k: [w0[k], w1[k]] for k in w0}}
+
+
 def cnn(arch, args, dev):
     torch.manual_seed(0)
     model = getattr(cnn_models, arch)(pretrained=False).to(dev).eval()
@@ -387,9 +418,14 @@ def main():
     ap.add_argument("--fused-only", choices=("mobilenet_v2", "efficientnet_b0"),
                     help="the fused executor of one config alone (profiling runs)")
     ap.add_argument("--streams", type=int, default=2, help="image chunks / streams (fused-only)")
+    ap.add_argument("--lstm-trace", type=int, default=0, metavar="CHUNKS",
+                    help="profiling mode: CHUNKS term-pair LSTM-650 chunks and their clocks")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = True
+    if args.lstm_trace:
+        print(json.dumps(lstm_trace(args.lstm_trace, dev)), flush=True)
+        return
     if args.fused_only:
         print(json.dumps(cnn_fused(args.fused_only, args.steps, args.warmup, args.batch, dev,
                                    args.streams)), flush=True)
