@@ -59,7 +59,7 @@
 #define C64_AB 0  // timing-only ablation builds (tools/variant1.sh); 0 = the product kernel
 #endif
 #ifndef C64_PF
-#define C64_PF 1  // substeps of fragment prefetch (1 or 2)
+#define C64_PF 2  // substeps of fragment prefetch (2: conv1 77 -> 73 us; residual forms equal)
 #endif
 #ifndef C64_PRIO
 #define C64_PRIO 0  // 1: s_setprio 1 for waves 4-7, 2: for waves 0-3 (A/B builds)
