@@ -7,7 +7,7 @@ for L in $LAYERS; do
   for F in "--no-out" "--residual"; do
     for v in default $VARS; do
       lib=""; [ "$v" != default ] && lib=$R/term-quantization_amd/lib/libtq_hip_$v.so
-      TQ_LIB_PATH=$lib timeout -k 10 120 python -u tools/conv_probe.py --layer $L --config 13 --codes 1 $F --iters 30 2>/dev/null | grep layer | sed "s/^/$F $v /" || exit 1
+      TQ_LIB_PATH=$lib timeout -k 10 120 python -u tools/conv_probe.py --layer $L --config 13 --codes 1 --nonneg $F --iters 30 2>/dev/null | grep layer | sed "s/^/$F $v /" || exit 1
     done
   done
 done
