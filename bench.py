@@ -60,7 +60,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--cpu-sample", type=int, default=64,
+    ap.add_argument("--cpu-sample", type=int, default=256,
                     help="images in the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--engine", choices=("mfma", "valu"), default="mfma",
@@ -324,7 +324,31 @@ def cpu_baseline(model_fp, qmodel, nimg):
                       "(oracle/tr_oracle.c) on every TR-layer activation split over %d threads + "
                       "torch-CPU fp32 conv (%d threads) on the fake-quantized tensors; weight TR "
                       "excluded (one-time conversion)" % (nimg, threads, threads),
-            "tr_op": cpu_tr_op_baseline(oracle)}
+            "tr_op": cpu_tr_op_baseline(oracle),
+            "python_restatements": cpu_python_baselines(oracle)}
+
+
+def cpu_python_baselines(oracle, nq=200000, nx=1 << 16):
+    """BASELINE.md C1 and C2 on one core: the pure-Python restatements of bit_utils.hese
+    (random q in [-511, 511], seed 0) and of the whole tr() (hese + the greedy group top-k,
+    g=8, k=12, on relu(N(0,1)) fp32 at sf=0.05, db=9) -- oracle.hese_py / oracle.tr_py, the
+    latter checked bit for bit against the C restatement on its sample here."""
+    rng = np.random.default_rng(0)
+    qs = rng.integers(-511, 512, nq).tolist()
+    t0 = time.perf_counter()
+    for q in qs:
+        oracle.hese_py(q)
+    t_hese = time.perf_counter() - t0
+    x = np.maximum(rng.standard_normal(nx, dtype=np.float32), 0)
+    t0 = time.perf_counter()
+    y = oracle.tr_py(x, 0.05, DB, 8, 12)
+    t_tr = time.perf_counter() - t0
+    ok = bool(np.array_equal(y.view(np.int32),
+                             oracle.tr(x.reshape(1, -1), 0.05, DB, 8, 12).reshape(-1).view(np.int32)))
+    return {"c1_hese_values_per_s": nq / t_hese, "c2_tr_elements_per_s": nx / t_tr,
+            "cores": 1, "kind": "port", "c2_matches_c_restatement": ok,
+            "sample": "C1: %d random q in [-511, 511] (seed 0), oracle.hese_py; C2: %d relu(N(0,1)) "
+                      "fp32, g=8 k=12 sf=0.05 db=%d, oracle.tr_py" % (nq, nx, DB)}
 
 
 def cpu_tr_op_baseline(oracle, n=1 << 24):

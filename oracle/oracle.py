@@ -94,6 +94,61 @@ def hese_masks(qs):
     return pos, neg
 
 
+def hese_py(number):
+    """Pure-Python restatement of bit_utils.hese (bit_utils.py:10-44): the bit windows
+    (b[i+1], b[i], b[i-1]) scanned from the top bit down -- 010 -> sign 2^i (and skip bit
+    i-1), 011 -> sign 2^(i+1), 110 -> -sign 2^i -- on Python ints instead of the reference's
+    binary strings.  BASELINE C1's single-core baseline (bench.py cpu_baseline)."""
+    sign = -1 if number < 0 else 1
+    q = -number if number < 0 else number
+    out = []
+    i = q.bit_length() - 1
+    while i >= 0:
+        if (q >> i) & 1:
+            above = (q >> (i + 1)) & 1
+            below = (q >> (i - 1)) & 1 if i > 0 else 0
+            if not above:
+                if below:
+                    out.append(sign * (1 << (i + 1)))
+                else:
+                    out.append(sign * (1 << i))
+                    i -= 1
+            elif not below:
+                out.append(-sign * (1 << i))
+        i -= 1
+    return out
+
+
+def tr_py(x, sf, bitwidth, group_size, num_keep_terms):
+    """Pure-Python restatement of the whole tr() on a flat float32 vector grouped by
+    consecutive elements (a (1, C) tensor): quantize as tr_cuda_kernel.cu:21-23 (fp32 |x| / sf,
+    + 0.5 in double, truncate, clamp to 2^b - 1), hese_py terms, the greedy per-group top-k of
+    :92-116 (largest |term| first, the lowest index on ties) and the fp32 rescale of :119-123.
+    BASELINE C2's single-core baseline; checked against ``tr`` (the C restatement)."""
+    x = np.asarray(x, dtype=np.float32).reshape(-1)
+    sf32 = np.float32(sf)
+    maxv = (1 << bitwidth) - 1
+    out = np.zeros_like(x)
+    for g0 in range(0, x.size, group_size):
+        terms = []
+        for v in x[g0:g0 + group_size]:
+            t = float(np.float32(abs(v)) / sf32) + 0.5
+            q = min(int(t) if t == t else 0, maxv)
+            terms.append(hese_py(-q if v < 0 else q))
+        idx = [0] * len(terms)
+        for _ in range(num_keep_terms):
+            best, bj = 0, 0
+            for j, tj in enumerate(terms):
+                if idx[j] < len(tj) and abs(tj[idx[j]]) > abs(best):
+                    best, bj = tj[idx[j]], j
+            if best == 0:
+                break
+            out[g0 + bj] += np.float32(best)
+            idx[bj] += 1
+        out[g0:g0 + group_size] *= sf32
+    return out
+
+
 def tr_layer_hese_len(q):
     """len(tr_layer.hese(q)) (tr_layer.py:9-41): runs of ones cost 2 terms, lone ones 1."""
     q = abs(int(q))

@@ -46,6 +46,33 @@ def test_oracle_term_order_matches_bit_utils():
     assert oracle.hese_terms(-5) == [-4, -1]
 
 
+def test_python_hese_restatement_matches_golden_and_c():
+    """oracle.hese_py (BASELINE C1's Python baseline) = the golden bit_utils.hese masks and
+    the C encoder's term lists (order and sign)."""
+    g = np.load(os.path.join(GOLDEN, "hese_bit_utils.npz"))
+    for q, p, n in zip(g["q"].tolist(), g["pos"].tolist(), g["neg"].tolist()):
+        terms = oracle.hese_py(q)
+        sp = sum(1 << (abs(t).bit_length() - 1) for t in terms if t > 0)
+        sn = sum(1 << (abs(t).bit_length() - 1) for t in terms if t < 0)
+        assert (sp, sn) == (p, n), q
+    rng = np.random.default_rng(3)
+    for q in list(range(-1100, 1100)) + rng.integers(-(1 << 22), 1 << 22, 500).tolist():
+        assert oracle.hese_py(q) == oracle.hese_terms(q), q
+
+
+@pytest.mark.parametrize("g,k", [(8, 12), (1, 3), (4, 5), (16, 20), (8, 0)])
+def test_python_tr_restatement_matches_c(g, k):
+    """oracle.tr_py (BASELINE C2's Python baseline) is bit-identical to the C restatement on a
+    flat (1, C) tensor, partial last group and clamped values included."""
+    rng = np.random.default_rng(g * 100 + k)
+    x = (rng.standard_normal(3000) * 3).astype(np.float32)
+    x[::97] = 0.0
+    x[5] = 1e9  # clamps to 2^b - 1
+    a = oracle.tr_py(x, 0.05, 9, g, k)
+    b = oracle.tr(x.reshape(1, -1), 0.05, 9, g, k).reshape(-1)
+    np.testing.assert_array_equal(a.view(np.int32), b.view(np.int32))
+
+
 def test_closed_form_hese_full_table_sha256():
     """Every q < 2^17 through the device closed form hashes to the bit_utils.hese table."""
     meta = json.load(open(os.path.join(GOLDEN, "hese_bit_utils_sha256.json")))
