@@ -44,9 +44,7 @@ const char *tq_last_error(void);
 /*
  * Diagnostics: the number of bounded in-kernel waits that ran out since the previous call --
  * the row-strip conv engine's team syncs (each one means a launch went on without confirming
- * that its LDS patch was staged, so its results are suspect) and the persistent
- * tq_lstm_seq2_f32 launch's grid barriers (a launch went on without every workgroup's h) --
- * then clears the count.
+ * that its LDS patch was staged, so its results are suspect) -- then clears the count.
  * Synchronous (waits for the device); `count` is a host pointer.  A healthy run reads 0.
  */
 int tq_sync_faults(uint32_t *count);
@@ -418,9 +416,7 @@ int tq_lstm_seq_f32(const float *gx, const float *w_hh, const float *b_hh, const
  * Two stacked LSTM layers' recurrences (TRLSTMLayer's LSTM-650: layer 0 from the term-pair
  * input projection, layer 1 untouched by the reference's TR) in wavefront order: launch s
  * runs layer 0's step s and layer 1's step s - 1 in one grid, steps + 1 dependent launches
- * in all -- or, where every workgroup can be resident at once (and the stream is not being
- * captured; TQ_LSTM_PERSIST=0 opts out), the same iterations in ONE cooperative launch with a
- * grid barrier between them (bit-identical outputs; timeouts counted by tq_sync_faults).  Layer 0 as tq_lstm_seq_f32 (gx0 [steps][batch][4 hidden] incl. b_ih0, w_hh0,
+ * in all.  Layer 0 as tq_lstm_seq_f32 (gx0 [steps][batch][4 hidden] incl. b_ih0, w_hh0,
  * b_hh0, h00, c00 -> out0, c_out0); layer 1 computes its own input projection per step:
  *   gates_t = (out0[t] W_ih1^T + b_ih1) + (h_{t-1} W_hh1^T + b_hh1)
  * from (h01, c01) -> out1 [steps][batch][hidden], c_out1.  Biases may be NULL.  fp32

@@ -80,12 +80,7 @@ const char* tq_last_error(void) { return g_err; }
 
 int tq_sync_faults(uint32_t* count) {
   if (count == nullptr) return fail(TQ_ERR_INVALID_ARGUMENT, "sync_faults: count is null");
-  const int rc = hip_status(tq::strip_sync_faults(count), "sync_faults");
-  if (rc != TQ_OK) return rc;
-  const unsigned lf = tq::lstm_persist_faults();
-  if (lf == ~0u) return fail(TQ_ERR_HIP, "sync_faults: persistent LSTM fault read failed");
-  *count += lf;
-  return TQ_OK;
+  return hip_status(tq::strip_sync_faults(count), "sync_faults");
 }
 
 int tq_tr_f32(const float* input, float* output, int64_t ndim, const int64_t* shape, float sf,

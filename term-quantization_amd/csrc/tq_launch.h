@@ -109,7 +109,6 @@ hipError_t launch_lstm_cell(const float* gx, const float* hh, float* c, float* h
 // A whole LSTM layer's recurrence: T fused step launches from one call (tq_lstm.hip)
 int64_t lstm_seq_workspace_bytes(int64_t B, int64_t H);
 bool lstm_seq2_supported(int64_t B, int64_t H);
-unsigned lstm_persist_faults();  // spin timeouts of the persistent seq2 launches (then reset)
 hipError_t launch_lstm_seq2(const float* gx0, const float* w_hh0, const float* b_hh0,
                             const float* h00, const float* c00, const float* w_ih1,
                             const float* b_ih1, const float* w_hh1, const float* b_hh1,

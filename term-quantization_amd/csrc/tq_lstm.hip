@@ -6,9 +6,6 @@
 // One launch per step instead of the ~8 point-wise torch kernels; fp32 like the reference's
 // cuDNN LSTM (its summation order is unpinned: DESIGN.md 3).
 #include <math.h>
-#include <stdlib.h>
-
-#include <mutex>
 
 #include "tq_launch.h"
 
@@ -407,285 +404,6 @@ __global__ __launch_bounds__(kStepThreads) void lstm_step2_kernel(LstmStep2Args 
     lstm2_role<P, true>(a.r[1], wg, a.B, a.H, a.nu, step2_lds);
 }
 
-// ---------------------------------------------------------------------------------------
-// The same wavefront recurrence in ONE cooperative launch (TQ_LSTM_PERSIST, default on where
-// the launch is possible): every workgroup of both roles stays resident for all T + 1
-// iterations, so its W rows are loaded into registers once instead of once per step, and the
-// per-step kernel boundary becomes a grid barrier.  The hand-off of h between iterations:
-// each workgroup's h stores complete (vmcnt(0)), its thread 0 releases at agent scope (the
-// XCD's L2 written back) and arrives on a counter, spins (agent-scope loads, bounded) until
-// every workgroup arrived, then acquires at agent scope (stale L2 lines invalidated) -- so the
-// next iteration's h rows are ordinary cached loads (one L2 miss per XCD, then L2 hits), not
-// the per-element agent-scope granules of the round-2 persistent kernel (26 us per step).
-// The counter is monotonic across launches (the host passes the value it starts from); a
-// spin that exhausts its bound sets a fault flag (tq_lstm_persist_faults) and the kernel
-// finishes without waiting, so it can never hang.  Same arithmetic as lstm_step2_kernel:
-// bit-identical outputs (tests/test_gpu_lstm.py).
-// ---------------------------------------------------------------------------------------
-struct LstmPersistArgs {
-  LstmRole r[2];  // w / b (and layer 1's w_ih / b_ih); the per-step pointers are derived here
-  const float *gx0, *h00, *c00, *h01, *c01;
-  float *out0, *out1, *cT0, *cT1;
-  unsigned* bar;    // [0] arrival counter, [1] fault flag
-  unsigned base;    // counter value when this launch starts
-  int T, B, H, nu, G;
-};
-
-// wait until every workgroup of the grid arrived at barrier `k` of this launch (thread 0's
-// `faulted`: this workgroup already timed out once and no longer waits)
-__device__ __forceinline__ void lstm_grid_barrier(const LstmPersistArgs& a, int k,
-                                                  bool& faulted) {
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's h stores are in L2
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = a.base + (unsigned)(k + 1) * gridDim.x;
-    unsigned spins = 0;
-    while (!faulted && (int)(__hip_atomic_load(a.bar, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      if (++spins > (1u << 18)) {  // a fraction of a second: never a hang
-        __hip_atomic_store(a.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        faulted = true;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-template <int P, bool X2>
-__device__ __forceinline__ void lstm2_persist_role(const LstmPersistArgs& pa, int wg,
-                                                   float* lds) {
-  constexpr int HP = 2 * kStepSeg * P;
-  const LstmRole& a = pa.r[X2 ? 1 : 0];
-  const int B = pa.B, H = pa.H, nu_max = pa.nu;
-  const int tid = threadIdx.x;
-  const int u0 = wg * nu_max;
-  const int nu = min(nu_max, H - u0);
-  float* hprev = lds;
-  float* xin = hprev + (int64_t)B * HP;
-  float* part_h = xin + (int64_t)B * HP;
-  float* part_x = part_h + (int64_t)4 * nu_max * B * kStepSeg;
-  const bool cell = tid < B * nu;
-  const int ct = cell ? tid : 0;
-  const int cb = ct / nu, cu = ct - (ct / nu) * nu;
-  float bpre[4], xbpre[4];
-#pragma unroll
-  for (int gi = 0; gi < 4; ++gi) {
-    const int col = gi * H + u0 + cu;
-    bpre[gi] = a.b ? a.b[col] : 0.0f;
-    xbpre[gi] = X2 && a.b_ih ? a.b_ih[col] : 0.0f;
-  }
-  float c = (X2 ? pa.c01 : pa.c00)[(int64_t)cb * H + u0 + cu];
-  // W rows into registers once for the whole sequence
-  const int r = tid / kStepSeg, s = tid % kStepSeg;
-  const bool dot = r < 4 * nu;
-  const int64_t wrow = dot ? (int64_t)((r / nu) * H + u0 + r % nu) * H : 0;
-  float2 wh[P], wx[X2 ? P : 1];
-#pragma unroll
-  for (int i = 0; i < P; ++i) {
-    const int j = 2 * (s + kStepSeg * i);
-    const bool ok = dot && j < H;
-    wh[i] = ok ? *reinterpret_cast<const float2*>(a.w + wrow + j) : make_float2(0.f, 0.f);
-    if (X2)
-      wx[i] = ok ? *reinterpret_cast<const float2*>(a.w_ih + wrow + j) : make_float2(0.f, 0.f);
-  }
-  const int64_t BH = (int64_t)B * H;
-  constexpr int JC = (HP + kStepThreads - 1) / kStepThreads;
-  bool faulted = false;
-  for (int it = 0; it <= pa.T; ++it) {
-    // iteration it: layer 0's step it, layer 1's step it - 1
-    const int t = X2 ? it - 1 : it;
-    if (t >= 0 && t < pa.T) {
-      const float* hsrc = X2 ? (t == 0 ? pa.h01 : pa.out1 + (t - 1) * BH)
-                             : (t == 0 ? pa.h00 : pa.out0 + (t - 1) * BH);
-      const float* xsrc = pa.out0 + t * BH;  // (X2) layer 0's output at step t
-      float gpre[4];
-#pragma unroll
-      for (int gi = 0; gi < 4; ++gi)
-        gpre[gi] = X2 ? 0.0f : pa.gx0[((int64_t)t * B + cb) * 4 * H + gi * H + u0 + cu];
-      const int nrow = X2 ? 2 * B : B;
-      for (int q0 = 0; q0 < nrow; q0 += kStageRows) {
-        float v[kStageRows][JC];
-#pragma unroll
-        for (int i = 0; i < kStageRows; ++i) {
-          const int q = min(q0 + i, nrow - 1);
-          const float* src = q < B ? hsrc + (int64_t)q * H : xsrc + (int64_t)(q - B) * H;
-#pragma unroll
-          for (int jj = 0; jj < JC; ++jj) {
-            const int j = tid + jj * kStepThreads;
-            const float x = src[min(j, H - 1)];
-            v[i][jj] = j < H ? x : 0.0f;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kStageRows; ++i) {
-          const int q = q0 + i;
-          if (q >= nrow) break;
-          float* dst = q < B ? hprev + q * HP : xin + (q - B) * HP;
-#pragma unroll
-          for (int jj = 0; jj < JC; ++jj) {
-            const int j = tid + jj * kStepThreads;
-            if (j < HP) dst[j] = v[i][jj];
-          }
-        }
-      }
-      __syncthreads();
-      if (dot) {
-        for (int bb = 0; bb < B; ++bb) {
-          const float2* hp = reinterpret_cast<const float2*>(hprev + bb * HP) + s;
-          float acc0 = 0.0f, acc1 = 0.0f;
-#pragma unroll
-          for (int i = 0; i < P; ++i) {
-            const float2 hv = hp[kStepSeg * i];
-            acc0 = fmaf(hv.x, wh[i].x, acc0);
-            acc1 = fmaf(hv.y, wh[i].y, acc1);
-          }
-          part_h[((int64_t)r * B + bb) * kStepSeg + s] = acc0 + acc1;
-          if (X2) {
-            const float2* xp = reinterpret_cast<const float2*>(xin + bb * HP) + s;
-            float x0 = 0.0f, x1 = 0.0f;
-#pragma unroll
-            for (int i = 0; i < P; ++i) {
-              const float2 xv = xp[kStepSeg * i];
-              x0 = fmaf(xv.x, wx[i].x, x0);
-              x1 = fmaf(xv.y, wx[i].y, x1);
-            }
-            part_x[((int64_t)r * B + bb) * kStepSeg + s] = x0 + x1;
-          }
-        }
-      }
-      __syncthreads();
-      if (cell) {
-        float gate[4];
-#pragma unroll
-        for (int gi = 0; gi < 4; ++gi) {
-          const int64_t pi = ((int64_t)(gi * nu + cu) * B + cb) * kStepSeg;
-          float sum = 0.0f;
-#pragma unroll
-          for (int k = 0; k < kStepSeg; ++k) sum += part_h[pi + k];
-          float gxv = gpre[gi];
-          if (X2) {
-            float xs = 0.0f;
-#pragma unroll
-            for (int k = 0; k < kStepSeg; ++k) xs += part_x[pi + k];
-            gxv = xs + xbpre[gi];
-          }
-          gate[gi] = gxv + (sum + bpre[gi]);
-        }
-        c = sigmoid_f(gate[1]) * c + sigmoid_f(gate[0]) * tanhf(gate[2]);
-        (X2 ? pa.out1 : pa.out0)[t * BH + (int64_t)cb * H + u0 + cu] =
-            sigmoid_f(gate[3]) * tanhf(c);
-      }
-    }
-    if (it < pa.T) lstm_grid_barrier(pa, it, faulted);
-  }
-  if (cell) (X2 ? pa.cT1 : pa.cT0)[(int64_t)cb * H + u0 + cu] = c;
-}
-
-template <int P>
-__global__ __launch_bounds__(kStepThreads) void lstm2_persist_kernel(LstmPersistArgs a) {
-  extern __shared__ float persist_lds[];
-  const int wg = (int)(blockIdx.x % a.G);
-  if (blockIdx.x < (unsigned)a.G)
-    lstm2_persist_role<P, false>(a, wg, persist_lds);
-  else
-    lstm2_persist_role<P, true>(a, wg, persist_lds);
-}
-
-// per (device, stream) barrier word pair and the counter value the next launch starts from
-struct LstmBarrier {
-  int dev;
-  hipStream_t stream;
-  unsigned* bar;
-  unsigned next;
-};
-std::mutex g_lstm_bar_mu;
-LstmBarrier g_lstm_bars[16];
-int g_lstm_nbars = 0;
-
-LstmBarrier* lstm_barrier_for(hipStream_t stream) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(g_lstm_bar_mu);
-  for (int i = 0; i < g_lstm_nbars; ++i)
-    if (g_lstm_bars[i].dev == dev && g_lstm_bars[i].stream == stream) return &g_lstm_bars[i];
-  if (g_lstm_nbars == 16) return nullptr;
-  unsigned* bar = nullptr;
-  if (hipMalloc(&bar, 2 * sizeof(unsigned)) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (hipMemsetAsync(bar, 0, 2 * sizeof(unsigned), stream) != hipSuccess) {
-    (void)hipFree(bar);
-    return nullptr;
-  }
-  g_lstm_bars[g_lstm_nbars] = LstmBarrier{dev, stream, bar, 0u};
-  return &g_lstm_bars[g_lstm_nbars++];
-}
-
-// 1: the persistent launch ran; 0: not possible here (capture, residency): use the step
-// launches; < 0: a launch error
-template <int P>
-int launch_lstm_persist2(const LstmStep2Args& s2, const float* gx0, const float* h00,
-                         const float* c00, const float* h01, const float* c01, float* out0,
-                         float* out1, float* cT0, float* cT1, int64_t T, hipStream_t stream) {
-  const char* env = getenv("TQ_LSTM_PERSIST");  // read per call: tests switch it
-  if (!(env && atoi(env) == 1)) return 0;  // (opt-in until measured on the GPU)
-  if (T > (1 << 20)) return 0;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
-    return 0;
-  constexpr int HP = 2 * kStepSeg * P;
-  const size_t lds = (size_t)lstm2_lds_floats(s2.B, HP, s2.nu) * sizeof(float);
-  const void* fn = reinterpret_cast<const void*>(&lstm2_persist_kernel<P>);
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-        hipSuccess)
-      return 0;
-    attr_set = true;
-  }
-  const int grid = 2 * s2.G;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kStepThreads, lds) !=
-          hipSuccess ||
-      (int64_t)per_cu * device_cus() < grid)
-    return 0;  // not every workgroup could be resident at once
-  LstmBarrier* lb = lstm_barrier_for(stream);
-  if (!lb) return 0;
-  LstmPersistArgs a = {};
-  a.r[0] = s2.r[0];
-  a.r[1] = s2.r[1];
-  a.gx0 = gx0;
-  a.h00 = h00;
-  a.c00 = c00;
-  a.h01 = h01;
-  a.c01 = c01;
-  a.out0 = out0;
-  a.out1 = out1;
-  a.cT0 = cT0;
-  a.cT1 = cT1;
-  a.bar = lb->bar;
-  a.base = lb->next;
-  a.T = (int)T;
-  a.B = s2.B;
-  a.H = s2.H;
-  a.nu = s2.nu;
-  a.G = s2.G;
-  void* args[] = {&a};
-  const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(grid), dim3(kStepThreads), args,
-                                                  (unsigned)lds, stream);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return 0;  // (the counter did not move)
-  }
-  lb->next += (unsigned)T * (unsigned)grid;
-  return 1;
-}
-
 // column pairs per thread of the two-layer kernel: 32 P >= H (0: H outside its domain)
 static int lstm2_pairs(int64_t H) {
   if (H < 2 || (H & 1)) return 0;
@@ -708,8 +426,6 @@ hipError_t launch_lstm_steps2(LstmStep2Args a, const float* gx0, const float* h0
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  if (launch_lstm_persist2<P>(a, gx0, h00, c00, h01, c01, out0, out1, cT0, cT1, T, stream) == 1)
-    return hipGetLastError();
   for (int64_t s = 0; s <= T; ++s) {
     const bool have0 = s < T, have1 = s >= 1;
     if (have0) {  // layer 0, step s
@@ -737,24 +453,6 @@ hipError_t launch_lstm_steps2(LstmStep2Args a, const float* gx0, const float* h0
 }
 
 }  // namespace
-
-// spin timeouts of the persistent launches so far on the current device (tests), reset to 0
-unsigned lstm_persist_faults() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return ~0u;
-  unsigned total = 0;
-  std::lock_guard<std::mutex> lk(g_lstm_bar_mu);
-  for (int i = 0; i < g_lstm_nbars; ++i) {
-    if (g_lstm_bars[i].dev != dev) continue;
-    unsigned f = 0;
-    if (hipMemcpy(&f, g_lstm_bars[i].bar + 1, sizeof(unsigned), hipMemcpyDeviceToHost) !=
-        hipSuccess)
-      return ~0u;
-    total += f;
-    (void)hipMemset(g_lstm_bars[i].bar + 1, 0, sizeof(unsigned));
-  }
-  return total;
-}
 
 bool lstm_seq2_supported(int64_t B, int64_t H) {
   const int64_t P = lstm2_pairs(H);

@@ -27,22 +27,19 @@ def _oracle_w(w, bits, g, k):
     return torch.from_numpy(oracle.tr(w.detach().cpu().contiguous().numpy(), sf, bits, g, k))
 
 
-@pytest.mark.parametrize("termpair,seq", [(False, None), (True, "1"), (True, "steps"),
-                                          (True, "layer"), (True, "0"), (True, "miopen")])
+@pytest.mark.parametrize("termpair,seq", [(False, None), (True, "1"), (True, "layer"),
+                                          (True, "0"), (True, "miopen")])
 def test_lstm650_tq_chunk_against_oracle(termpair, seq, monkeypatch):
     """seq (term-pair path): "1" (default) = both layers in wavefront order, T + 1 launches
     (tq_lstm_seq2_f32), "layer" = each layer's recurrence from one call (tq_lstm_seq_f32,
     TQ_LSTM_WAVE=0), "0" = per-step launches (a GEMM + tq_lstm_cell_f32 per step, MIOpen for
-    layer 1), "miopen" = the one-call recurrence for layer 0, MIOpen above, "steps" = the
-    wavefront as T + 1 step launches instead of one persistent launch (TQ_LSTM_PERSIST=0)."""
+    layer 1), "miopen" = the one-call recurrence for layer 0, MIOpen above."""
     import evaluate_lstm
     import tq_native
     if seq == "miopen":
         monkeypatch.setenv("TQ_LSTM_UPPER", "miopen")
     elif seq == "layer":
         monkeypatch.setenv("TQ_LSTM_WAVE", "0")
-    elif seq == "steps":
-        monkeypatch.setenv("TQ_LSTM_PERSIST", "0")
     elif seq is not None:
         monkeypatch.setenv("TQ_LSTM_SEQ", seq)
     tq_native.sync_faults()
@@ -116,48 +113,3 @@ def test_lstm650_tq_chunk_against_oracle(termpair, seq, monkeypatch):
     assert bool((ratio <= 1.0).all()), float(ratio.max())
     assert float((hn.cpu().double() - hr).abs().max()) <= 1e-5
     assert float((cn.cpu().double() - cr).abs().max()) <= 1e-5 * max(1.0, float(cr.abs().max()))
-    assert tq_native.sync_faults() == 0
-
-
-@pytest.mark.parametrize("steps,batch,hidden", [(35, 10, 650), (1, 10, 650), (2, 1, 650),
-                                                (100, 23, 650), (7, 4, 256), (9, 3, 1024)])
-def test_lstm_seq2_persistent_is_bit_identical_to_step_launches(steps, batch, hidden,
-                                                                monkeypatch):
-    """The persistent cooperative launch of tq_lstm_seq2_f32 (W rows in registers for the
-    whole sequence, a grid barrier per iteration) gives the step launches' bits: both
-    layers' outputs and final cell states, over sequence lengths 1..100, batch 1..23, hidden
-    256 / 650 / 1024 (1024: too many registers for every workgroup to be resident, so both
-    runs take the step launches), three calls in a row on one stream (the barrier counter
-    carries over), no bounded wait running out."""
-    import tq_native
-    tq_native.sync_faults()
-    g = torch.Generator().manual_seed(steps * 1000 + batch + hidden)
-    H = hidden
-
-    def rnd(*shape, s=0.1):
-        return (torch.randn(*shape, generator=g) * s).to(DEV).contiguous()
-    gx0 = rnd(steps, batch, 4 * H, s=0.5)
-    w_hh0, w_ih1, w_hh1 = rnd(4 * H, H), rnd(4 * H, H), rnd(4 * H, H)
-    b_hh0, b_ih1, b_hh1 = rnd(4 * H), rnd(4 * H), rnd(4 * H)
-    h00, c00, h01, c01 = rnd(batch, H, s=0.3), rnd(batch, H, s=0.3), rnd(batch, H, s=0.3), \
-        rnd(batch, H, s=0.3)
-
-    def run():
-        out0 = torch.full((steps, batch, H), float("nan"), device=DEV)
-        out1 = torch.full((steps, batch, H), float("nan"), device=DEV)
-        cT0 = torch.full((batch, H), float("nan"), device=DEV)
-        cT1 = torch.full((batch, H), float("nan"), device=DEV)
-        tq_native.lstm_seq2(gx0, w_hh0, b_hh0, h00, c00, w_ih1, b_ih1, w_hh1, b_hh1, h01,
-                            c01, out0, out1, cT0, cT1)
-        torch.cuda.synchronize()
-        return [t.cpu() for t in (out0, out1, cT0, cT1)]
-    monkeypatch.setenv("TQ_LSTM_PERSIST", "0")
-    ref = run()
-    assert not any(torch.isnan(t).any() for t in ref)
-    monkeypatch.setenv("TQ_LSTM_PERSIST", "1")
-    for _ in range(3):
-        got = run()
-        for a, b in zip(got, ref):
-            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
-    assert tq_native.sync_faults() == 0
-
