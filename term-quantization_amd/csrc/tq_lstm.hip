@@ -56,7 +56,9 @@ hipError_t launch_lstm_cell(const float* gx, const float* hh, float* c, float* h
 // LDS, 16 threads per gate row each take a 1/16 segment of the row's dot products for every
 // batch row, and its cell threads finish the units.  The kernel boundary is the step's grid-
 // wide hand-off.  (A persistent single-launch version exchanging h through agent-scope
-// granules measured 26 us per step -- slower than these launches: DESIGN.md 7.)
+// granules measured 26 us per step, and a cooperative two-layer one with W in registers and
+// an agent-scope release/acquire grid barrier ~42 us per iteration -- both slower than these
+// launches: DESIGN.md 7, profiles/r05_lstm_persistent_ab.txt.)
 // fp32 throughout, like the reference's cuDNN LSTM; per dot product 16 partial sums of
 // consecutive terms, added in a fixed order.
 // ---------------------------------------------------------------------------------------
