@@ -1,6 +1,7 @@
 #!/bin/bash
 # Ring-engine phase-shift probe (RING_AB=12 build): workgroups with one tile fewer, every other
 # one, start TQ_AB x ~3.4 us late.  Usage: bash tools/gpu_ring_phase.sh "<layers>" "<delays>"
+# (RING_AB=12 was a timing-only build option, reverted after this probe: profiles/r05_ring_epilogue_probes.txt)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; LAYERS=$1; DELAYS=$2
 for L in $LAYERS; do

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Ring-engine rows-per-tile probe (TQ_RING_R): bash tools/gpu_ring_rows.sh "<layer:R,R..> ..."
+# (TQ_RING_R was an A/B override, reverted after this probe: profiles/r05_ring_rows_probe.txt)
 set -u
 R0=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R0"
 for spec in "$@"; do
