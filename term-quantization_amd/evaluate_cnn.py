@@ -100,7 +100,8 @@ def setup(args):
     """Device, process group, loader, criterion and the fp32 model.
 
     One process per device under torchrun: RCCL ("nccl") on GPUs, gloo on the CPU
-    (``--gpu -1``, or no GPU present).  Every rank evaluates its own strided share of the
+    (``--gpu -1``, or no GPU present); TQ_DIST_BACKEND=gloo selects gloo on GPUs too (ranks
+    sharing one device, as tests/test_gpu_dist.py runs them: RCCL takes one rank per GPU).  Every rank evaluates its own strided share of the
     batches -- the synthetic set and the ImageFolder alike (util.StridedBatchSampler) -- so
     the all-reduced counters cover each sample exactly once."""
     global val_loader, criterion
@@ -119,6 +120,8 @@ def setup(args):
         dev = torch.device('cuda', args.gpu)
     if world > 1:
         if use_cpu:
+            dist.init_process_group('gloo')
+        elif os.environ.get('TQ_DIST_BACKEND', 'nccl') == 'gloo':
             dist.init_process_group('gloo')
         else:
             dist.init_process_group('nccl', device_id=dev)

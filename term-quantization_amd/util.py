@@ -168,8 +168,8 @@ def validate(val_loader, model, criterion, args, verbose=True, pct=1.0):
         dev = torch.device('cuda', args.gpu) if args.gpu is not None else torch.device('cpu')
         t = torch.tensor([loss_sum], dtype=torch.float64, device=dev)
         c = torch.tensor([correct, count], dtype=torch.int64, device=dev)
-        dist.all_reduce(t)
-        dist.all_reduce(c)
+        all_reduce_sum(t)
+        all_reduce_sum(c)
         loss_sum = float(t.item())
         correct, count = (int(v) for v in c.tolist())
     loss = loss_sum / max(count, 1)
@@ -194,6 +194,18 @@ def accuracy(output, target, topk=1):
         return 100.0 * hits.float().mean().item()
 
 
+def all_reduce_sum(t):
+    """In-place sum over the ranks: RCCL on device tensors; under gloo (CPU ranks, or ranks
+    sharing one GPU: evaluate_cnn TQ_DIST_BACKEND=gloo) a device tensor goes through a host
+    copy."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t)
+
+
 def allreduce_histograms(model):
     """Sum every TR layer's calibration histogram over all ranks (one collective for the
     whole model), so each rank's mse_profile sees the global activation distribution.
@@ -205,6 +217,6 @@ def allreduce_histograms(model):
     if not quants:
         return
     flat = torch.stack([q.hist_bins for q in quants])
-    dist.all_reduce(flat)
+    all_reduce_sum(flat)
     for q, h in zip(quants, flat):
         q.hist_bins.copy_(h)
