@@ -51,7 +51,17 @@
 #define RING_DMA_LATE 0  // 1: a step's DMA issued after its first substep (A/B builds)
 #endif
 
+#ifndef RING_TRACE
+#define RING_TRACE 0  // timing-only builds: per-tile phase stamps of wave 0 (tools/ring_trace.py)
+#endif
+
 namespace tq {
+
+#if RING_TRACE
+// [workgroup][tile of its stream < 8][tile start, first barrier passed, K loop done, epilogue
+// issued] (s_memrealtime ticks, 100 MHz) of the last traced launch
+__device__ unsigned long long g_ring_trace[1024 * 8 * 4];
+#endif
 
 namespace {
 
@@ -402,6 +412,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
           if (FLUSH) acci[bm][bn][r] = 0;
         }
     const bool has_next = seq + 1 < n_seq;
+#if RING_TRACE
+    unsigned long long tr_s = __builtin_amdgcn_s_memrealtime(), tr_b = 0, tr_k = 0;
+#endif
     int since = 0;
     for (int c = c_lo; c < c_hi; ++c) {
       const bool last_chunk = c + 1 == c_hi;
@@ -430,6 +443,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
         }();
         if constexpr (RING_AB != 1) TQ_WAIT_VM(nyoung);  // (RING_AB 1: timing only, no wait)
         if constexpr (RING_AB != 5) __builtin_amdgcn_s_barrier();  // (5: timing only)
+#if RING_TRACE
+        if (t == 0 && c == c_lo) tr_b = __builtin_amdgcn_s_memrealtime();
+#endif
         asm volatile("" ::: "memory");
         // (2) weight image of step s+NR-1 into the slot of step s-1; one patch piece of the
         // next chunk (RING_DMA_LATE: after substep 0's MFMAs, so the matrix cores restart
@@ -522,6 +538,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
 
     // ---- a split tile (SK): partial sums to this workgroup's slab; the last contributor adds
     // the others' and runs the epilogue (RingSk)
+#if RING_TRACE
+    tr_k = __builtin_amdgcn_s_memrealtime();
+#endif
     bool emit = true;
     if constexpr (SK) {
       if (c_lo != 0 || c_hi != nch) {
@@ -706,6 +725,15 @@ __global__ __launch_bounds__(64 * NW, 2) void conv2d_tp_ring_kernel(ConvArgs a, 
       }
     }
 
+#if RING_TRACE
+    if (tid == 0 && blockIdx.x < 1024 && seq < 8) {
+      unsigned long long* r = g_ring_trace + ((int64_t)blockIdx.x * 8 + seq) * 4;
+      r[0] = tr_s;
+      r[1] = tr_b;
+      r[2] = tr_k;
+      r[3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     if (!has_next) break;
     // ---- next tile: its patch chunk 0 and weight steps 0/1 are already staged or in flight
     ++seq;
@@ -952,5 +980,17 @@ hipError_t launch_conv2d_ring(const ConvArgs& a, hipStream_t stream) {
   if (!ring_plan<8, 64>(a, &pl)) return hipErrorInvalidValue;
   return launch_ring_shape<8, 64>(a, pl, 1, stream);
 }
+
+#if RING_TRACE
+extern "C" int tq_ring_trace_read(void* dst, int64_t n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_ring_trace), (size_t)n * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int tq_ring_trace_clear() {
+  static unsigned long long zero[1024 * 8 * 4];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ring_trace), zero, sizeof(zero), 0,
+                                hipMemcpyHostToDevice);
+}
+#endif
 
 }  // namespace tq
