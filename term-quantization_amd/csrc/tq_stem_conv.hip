@@ -54,11 +54,20 @@
 #ifndef STEM_CARRY
 #define STEM_CARRY 1  // 1: a tile's first conv row carried from the tile above (one strip per wave)
 #endif
+#ifndef STEM_TRACE
+#define STEM_TRACE 0  // timing-only builds: per-tile phase stamps of wave 0 (tools/stem_trace.py)
+#endif
 #ifndef STEM_PF
 #define STEM_PF 0  // 1: the next K-step's input slices read during this step's MFMAs
 #endif
 
 namespace tq {
+
+#if STEM_TRACE
+// [workgroup][tile of its run < 16][top, barrier A passed, barrier B passed, tile done]
+// (s_memrealtime ticks, 100 MHz) of the last traced launch
+__device__ unsigned long long g_stem_trace[1024 * 16 * 4];
+#endif
 
 namespace {
 
@@ -213,6 +222,9 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   f32x4 carry[4];
   int prev_tile = -2, prev_kx = 0;
   for (int tile = t_begin; tile < t_end; ++tile, ++it) {
+#if STEM_TRACE
+    const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int n = tile / tpi;
     const int py0 = (tile - n * tpi) * TP;
     {
@@ -231,6 +243,9 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       if (lane == 0) atomicMax(&tile_max[it & 1], lm);
     }
     __syncthreads();  // A: the previous tile's s2d rows are no longer read, tile max is final
+#if STEM_TRACE
+    const unsigned long long tr1 = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t mbits = tile_max[it & 1];
     int kx = 0;  // all-zero or non-finite tiles stay unscaled
     if (mbits != 0u && mbits < 0x7f800000u) {
@@ -242,6 +257,9 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
     if (STEM_AB != 3) commit(kx);  // (3: timing only, no input staging)
     if (tid == 0) tile_max[(it + 1) & 1] = 0u;
     __syncthreads();  // B
+#if STEM_TRACE
+    const unsigned long long tr2 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (STEM_AB != 3 && tile + 1 < t_end) prefetch(tile + 1);
 
     for (int b = wave; b < nb; b += ONE ? nb : kStemThreads / 64) {
@@ -477,6 +495,15 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       emit_pool(TP - 1, run, y[0]);
       }
     }
+#if STEM_TRACE
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && it < 16) {
+      unsigned long long* r = g_stem_trace + ((int64_t)blockIdx.x * 16 + it) * 4;
+      r[0] = tr0;
+      r[1] = tr1;
+      r[2] = tr2;
+      r[3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     prev_tile = tile;
     prev_kx = kx;
   }
@@ -537,5 +564,12 @@ hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream) {
   }
   return narrow ? launch_stem_tp<2, 3>(a, stream) : launch_stem_tp<2, 4>(a, stream);
 }
+
+#if STEM_TRACE
+extern "C" int tq_stem_trace_read(void* dst, int64_t n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stem_trace), (size_t)n * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // namespace tq
