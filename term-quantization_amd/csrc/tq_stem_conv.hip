@@ -67,6 +67,8 @@ namespace tq {
 // [workgroup][tile of its run < 16][top, barrier A passed, barrier B passed, tile done]
 // (s_memrealtime ticks, 100 MHz) of the last traced launch
 __device__ unsigned long long g_stem_trace[1024 * 16 * 4];
+// [workgroup][tile < 16][wave][after the prefetch issue, after pass 0, tile done]
+__device__ unsigned long long g_stem_trace_waves[1024 * 16 * 8 * 3];
 #endif
 
 namespace {
@@ -261,6 +263,10 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
     const unsigned long long tr2 = __builtin_amdgcn_s_memrealtime();
 #endif
     if (STEM_AB != 3 && tile + 1 < t_end) prefetch(tile + 1);
+#if STEM_TRACE
+    const unsigned long long trw0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long trw1 = 0;
+#endif
 
     for (int b = wave; b < nb; b += ONE ? nb : kStemThreads / 64) {
       const int c0 = 14 * b - 1;  // first conv column of the strip
@@ -469,6 +475,9 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll 1
         for (int p = 0; p < TP / 2; ++p) {
           conv_rows(std::integral_constant<int, 4>(), 4 * p + 1, y);
+#if STEM_TRACE
+          if (p == 0) trw1 = __builtin_amdgcn_s_memrealtime();
+#endif
           // pool row 2p: rr 4p (carry), 4p + 1, 4p + 2; pool row 2p + 1: rr 4p + 2 .. 4p + 4
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(carry[mb], y[0][mb]);
@@ -502,6 +511,13 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       r[1] = tr1;
       r[2] = tr2;
       r[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024 && it < 16) {
+      unsigned long long* rw =
+          g_stem_trace_waves + (((int64_t)blockIdx.x * 16 + it) * 8 + (threadIdx.x >> 6)) * 3;
+      rw[0] = trw0;
+      rw[1] = trw1;
+      rw[2] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     prev_tile = tile;
@@ -566,6 +582,10 @@ hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream) {
 }
 
 #if STEM_TRACE
+extern "C" int tq_stem_trace_waves_read(void* dst, int64_t n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stem_trace_waves), (size_t)n * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
 extern "C" int tq_stem_trace_read(void* dst, int64_t n) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stem_trace), (size_t)n * 8, 0,
                                   hipMemcpyDeviceToHost);

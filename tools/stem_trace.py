@@ -46,6 +46,14 @@ def main():
         v = d[:, :, i][used]
         print("%-40s mean %6.2f us  max %6.2f  total per workgroup %7.1f us" % (
             nm, v.mean(), v.max(), v.sum() / used.any(axis=1).sum()))
+    wv = np.zeros((1024, 16, 8, 3), dtype=np.uint64)
+    lib.tq_stem_trace_waves_read.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    assert lib.tq_stem_trace_waves_read(wv.ctypes.data, wv.size) == 0
+    wa = wv.astype(np.int64)[used]  # [tiles, 8 waves, 3 stamps]
+    b = t[used][:, 2][:, None]      # barrier B passed (wave 0)
+    for k, nm in enumerate(["after the prefetch issue", "after pass 0", "tile done"]):
+        print("per wave, %-26s (us after barrier B): %s" % (
+            nm, np.round(((wa[:, :, k] - b) / 100.0).mean(0), 2).tolist()))
     print("tiles per workgroup %s, span %.1f us" % (np.bincount(used.sum(axis=1))[1:].tolist(),
                                                    (t[used][:, 3].max() - base) / 100.0))
 
