@@ -1,5 +1,5 @@
-# (STEM_PRIO was a timing-only build option, reverted after this probe: profiles/r05_stem_trace.txt)
 #!/bin/bash
+# (STEM_PRIO was a timing-only build option, reverted after this probe: profiles/r05_stem_trace.txt)
 # Stem wave-priority A/B (STEM_PRIO variant builds sp1 / sp2, all with STEM_TRACE): per-tile
 # phases + per-wave lag (tools/stem_trace.py) and kernel time (tools/stem_probe.py), two rounds.
 set -u
