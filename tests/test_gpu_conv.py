@@ -230,3 +230,26 @@ def test_termpair_resnet_layer1_full_batch(engine):
     y_ref, mag, _ = _ref(x[idx].cpu(), w, None, 0.01, layer.w_sf, 9, 3, 9, 8, 12, 1, 1, 1)
     err = (y[idx].double().cpu() - y_ref).abs()
     assert bool((err <= RTOL * torch.maximum(y_ref.abs(), mag) + 1e-30).all())
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_termpair_conv_random_sweep(seed, engine):
+    """Seeded random conv shapes (kernel 1-7, stride 1-2, padding, dilation 1-2, ragged
+    channels, bias, NCHW / channels_last) and TR settings (group 1-32, kept terms, data
+    terms) through both engines, each within the 1e-5 bound of conv2d of the oracle's TR'd
+    tensors."""
+    rng = np.random.default_rng(2000 + seed)
+    ksz = int(rng.choice([1, 3, 5, 7]))
+    dil = int(rng.choice([1, 1, 2])) if ksz > 1 else 1
+    stride = int(rng.choice([1, 2]))
+    pad = int(rng.integers(0, ksz // 2 * dil + 1))
+    span = dil * (ksz - 1) + 1
+    h = int(rng.integers(max(span - 2 * pad, 1), 16))
+    w_ = int(rng.integers(max(span - 2 * pad, 1), 16))
+    c = int(rng.integers(1, 97))
+    cout = int(rng.integers(1, 97))
+    g = int(rng.choice([1, 2, 4, 8, 16, 32]))
+    k = int(rng.integers(1, 2 * g + 2))
+    dt = int(rng.integers(1, 5))
+    _run(int(rng.integers(1, 4)), c, h, w_, cout, ksz, stride, pad, dil, bool(rng.random() < 0.5),
+         bool(rng.random() < 0.5), seed=seed, dt=dt, g=g, k=k, engine=engine)

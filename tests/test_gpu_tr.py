@@ -207,3 +207,43 @@ def test_act_codes_near_midpoints():
         exp = oracle.tr(x.reshape(1, -1, 1, 1), sf, 14, 1, 3).reshape(16, 64)
         got = codes.cpu().numpy().reshape(16, 64).astype(np.float32) * np.float32(sf)
         np.testing.assert_array_equal(got, exp)
+
+
+def _random_case(rng):
+    """One seeded random TR case: shape (rank 2-4; ragged last groups half the time), group
+    (<= 32, the reference's limit), kept terms, bit width, scale and a value mix with ties,
+    tails and specials."""
+    g = int(rng.choice([1, 2, 3, 4, 8, 16, 32]))
+    k = int(rng.integers(0, 3 * g + 1))
+    bw = int(rng.integers(1, 17))
+    c = g * int(rng.integers(1, max(2, 256 // g))) + (int(rng.integers(0, g)) if rng.random() < 0.5 else 0)
+    rank = int(rng.integers(2, 5))
+    shape = (int(rng.integers(1, 9)), c) + tuple(int(rng.integers(1, 13)) for _ in range(rank - 2))
+    kind = int(rng.integers(0, 4))
+    n = int(np.prod(shape))
+    if kind == 0:
+        x = rng.standard_normal(n) * float(10.0 ** rng.uniform(-3, 3))
+    elif kind == 1:
+        x = rng.laplace(size=n) * float(10.0 ** rng.uniform(-2, 2))
+    elif kind == 2:
+        x = np.maximum(rng.standard_normal(n), 0.0)  # post-ReLU activations
+    else:
+        x = (rng.integers(-2 ** bw, 2 ** bw, n) + rng.choice([0.0, 0.5], n)).astype(np.float64)
+    qmax = float(2 ** bw - 1) if bw else 1.0
+    if kind == 3:
+        sf = float(rng.choice([1.0, 0.5, 0.25]))  # exact midpoints of the quantizer
+    else:
+        sf = float(np.abs(x).max()) / qmax * float(rng.choice([1.0, 0.5, 2.0])) or 1.0
+    special = rng.random(n) < 0.01
+    x[special] = rng.choice([0.0, -0.0, np.inf, -np.inf, np.nan, 1e30], int(special.sum()))
+    dtype = np.float64 if rng.random() < 0.25 else np.float32
+    return x.reshape(shape).astype(dtype), sf, bw, g, k
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_tr_random_sweep(seed):
+    """Seeded random sweep over shapes, groups, kept terms, bit widths 1-16, fp32 / fp64,
+    scales (incl. exact quantizer midpoints) and special values: bit-exact against the
+    oracle (the reference's tr kernel, kernels/tr_cuda_kernel.cu, restated in oracle/)."""
+    x, sf, bw, g, k = _random_case(np.random.default_rng(1000 + seed))
+    _check(x, sf, bw, g, k)
