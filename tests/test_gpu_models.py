@@ -307,3 +307,74 @@ def test_dw_fast_epilogue_bit_identical(cfg, form, monkeypatch):
     assert torch.equal(outs[0], outs[1])
     if form != "swish_out":
         assert (outs[0] != -1).all()  # every code written, pad channels included
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_depthwise_termpair_random_sweep(seed):
+    """Seeded random depthwise convs (channels 1-200, kernel 3/5, stride 1/2, padding or
+    EfficientNet static "same", bias, NCHW / channels_last, odd maps) against the fp64
+    depthwise conv of the oracle's TR'd tensors."""
+    rng = np.random.default_rng(3000 + seed)
+    c = int(rng.integers(1, 201))
+    k = int(rng.choice([3, 5]))
+    s = int(rng.choice([1, 2]))
+    same = bool(rng.random() < 0.3)
+    p = int(rng.integers(0, k // 2 + 1))
+    hw = int(rng.integers(k, 21))
+    bias = bool(rng.random() < 0.5)
+    torch.manual_seed(3000 + seed)
+    if same:
+        conv = Conv2dStaticSamePadding(c, c, k, stride=s, groups=c, bias=bias, image_size=hw)
+    else:
+        conv = nn.Conv2d(c, c, k, s, p, groups=c, bias=bias)
+    w = conv.weight.detach().clone()
+    b = conv.bias.detach().clone() if bias else None
+    layer = tr_layer.TRConv2dLayer(conv.to(DEV), 9, 3, 16, 1, 16)
+    assert layer.mode == "depthwise"
+    layer.input_quant.tracking = False
+    layer.input_quant.sf = 0.02
+    x = torch.relu(torch.randn(int(rng.integers(1, 4)), c, hw, hw))
+    xd = x.to(DEV)
+    if rng.random() < 0.5:
+        xd = xd.to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = layer(xd)
+    xq = _tr_x(x, 0.02, 9, 3)
+    wq = torch.from_numpy(oracle.tr(w.numpy(), layer.w_sf, 16, 1, 16)).double()
+    if same:
+        xq = conv.static_padding.cpu()(xq)
+    ref = F.conv2d(xq, wq, b.double() if bias else None, s, conv.padding, 1, c)
+    mag = F.conv2d(xq.abs(), wq.abs(), None, s, conv.padding, 1, c)
+    assert y.shape == ref.shape
+    _check(y, ref, mag)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_linear_termpair_random_sweep(seed):
+    """Seeded random TRLinearLayer(quantize_input=True) shapes (in 1-700, out 1-400, 2-D / 3-D
+    inputs) and TR settings (group 1-16, kept terms, data terms) against xq @ wq^T + b in
+    fp64 with the oracle's TR'd operands."""
+    rng = np.random.default_rng(4000 + seed)
+    fin, fout = int(rng.integers(1, 701)), int(rng.integers(1, 401))
+    g = int(rng.choice([1, 2, 4, 8, 16]))
+    k = int(rng.integers(1, 2 * g + 2))
+    dt = int(rng.integers(1, 9))
+    torch.manual_seed(4000 + seed)
+    lin = nn.Linear(fin, fout)
+    w = lin.weight.detach().clone()
+    b = lin.bias.detach().clone()
+    layer = tr_layer.TRLinearLayer(lin.to(DEV), 8, dt, 8, g, k, quantize_input=True)
+    assert layer.termpair
+    layer.input_quant.tracking = False
+    layer.input_quant.sf = 0.01
+    shape = (int(rng.integers(1, 40)), fin) if rng.random() < 0.5 else \
+        (int(rng.integers(1, 12)), int(rng.integers(1, 12)), fin)
+    x = torch.randn(*shape)
+    with torch.no_grad():
+        y = layer(x.to(DEV))
+    xq = _tr_x(x, 0.01, 8, dt)
+    wq = torch.from_numpy(oracle.tr(w.numpy(), layer.w_sf, 8, g, k)).double()
+    ref = xq @ wq.t() + b.double()
+    mag = xq.abs() @ wq.abs().t()
+    assert y.shape == shape[:-1] + (fout,)
+    _check(y, ref, mag)
