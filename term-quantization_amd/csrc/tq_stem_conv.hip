@@ -147,7 +147,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   // (3W floats).  The s2d halo columns (input columns outside the image) stay zero.
   constexpr int ROWS = 2 * (2 * TP + 4);
   constexpr int RPW = (ROWS + 7) / 8;
-  // QMAX float4 per lane and input row: W <= 64 * QMAX * 4 / 3 (3: W <= 256, 4: W <= 340)
+  // QMAX float4 per lane and input row: W <= 64 * QMAX * 4 / 3 (3: W <= 256, 4: W <= 340,
+  // 6: W <= 512; the launcher checks it)
   const int f4n = 3 * a.W / 4;
   for (int i = tid; i < (2 * TP + 4) * sc * 3; i += kStemThreads)
     reinterpret_cast<float4*>(xs)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -532,6 +533,7 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
   int64_t bytes =
       kStemWBytes + (int64_t)(2 * TP + 4) * sc * 12 * 4 + (kStemThreads / 64) * 7 * 64 * 4;
   if (bytes > kStemDynLds) return hipErrorInvalidConfiguration;
+  if (3 * a.W / 4 > 64 * QMAX) return hipErrorInvalidValue;  // an input row per lane group
   PoolArgs b = a;  // the epilogue code tables when they fit
   const int64_t lut = ((int64_t)(a.lut_a + a.lut_b) * 2 + 15) / 16 * 16;
   if (bytes + lut <= kStemDynLds) {
@@ -574,6 +576,9 @@ hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream) {
   static const char* tp = getenv("TQ_STEM_TP");  // A/B override (tools only)
   const bool narrow = 3 * a.W <= 64 * 3 * 4;  // every input row in 3 float4 per lane
+  // W > 340: 6 float4 per lane (the 4-float4 form dropped the input columns past 340); such
+  // a tile never fits four pool rows in the LDS
+  if (3 * a.W > 64 * 4 * 4) return launch_stem_tp<2, 6>(a, stream);
   if (!(tp && atoi(tp) == 2)) {
     const hipError_t e = narrow ? launch_stem_tp<4, 3>(a, stream) : launch_stem_tp<4, 4>(a, stream);
     if (e != hipErrorInvalidConfiguration) return e;

@@ -36,18 +36,38 @@ def _bn_coefs(seed):
 def test_stem_conv_pool_matches_fp64(n, h, w, fmt, xs):
     """xs scales the N(0,1) input: the kernel's per-tile power-of-two input scaling keeps the
     fp16 split in range for inputs far from unit scale."""
-    torch.manual_seed(h + w)
+    _stem_case(n, h, w, fmt, xs, h + w, (0.05, 9, 3))
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_stem_conv_pool_random_sweep(seed):
+    """Seeded random stem shapes (H, W multiples of 4, W up to 448 -- one or two strips per
+    wave, partial last tiles, narrow maps with idle waves), input scales 1e-4..1e4, code
+    format and TR settings (sf, bit width 6-11, data terms 1-4)."""
+    rng = np.random.default_rng(5000 + seed)
+    h = 4 * int(rng.integers(2, 59))
+    w = 4 * int(rng.integers(2, 113))
+    fmt = torch.float16 if rng.random() < 0.7 else torch.int16
+    xs = float(10.0 ** rng.uniform(-4, 4))
+    quant = (float(10.0 ** rng.uniform(-2.5, -0.5)), int(rng.integers(6, 12)),
+             int(rng.integers(1, 5)))
+    _stem_case(int(rng.integers(1, 4)), h, w, fmt, xs, 5000 + seed, quant)
+
+
+def _stem_case(n, h, w, fmt, xs, seed, quant):
+    sf, bw, dt = quant
+    torch.manual_seed(seed)
     x = (torch.randn(n, 3, h, w) * xs).contiguous(memory_format=torch.channels_last)
     wt = torch.empty(64, 3, 7, 7)
     nn.init.kaiming_normal_(wt, mode="fan_out", nonlinearity="relu")
-    sc, sh = _bn_coefs(h)
+    sc, sh = _bn_coefs(seed)
     ho, wo = h // 4, w // 4
     out = torch.full((n, 64, ho, wo), float("nan"), device=DEV).contiguous(
         memory_format=torch.channels_last)
     codes = torch.zeros((n, ho, wo, 64), dtype=fmt, device=DEV)
     wsplit = tq_ops.pack_stem_weight(wt.to(DEV))
     tq_native.stem_conv_pool_encode(x.to(DEV), wsplit, sc.to(DEV), sh.to(DEV), out,
-                                    codes_a=codes, quant_a=(0.05, 9, 3))
+                                    codes_a=codes, quant_a=(sf, bw, dt))
     got = out.cpu().double()
     # fp64 reference: conv -> BN (the fp32 coefficients) -> ReLU -> max-pool
     z = F.conv2d(x.double(), wt.double(), None, 2, 3)
@@ -59,8 +79,8 @@ def test_stem_conv_pool_matches_fp64(n, h, w, fmt, xs):
     assert not torch.isnan(got).any()
     assert bool((err <= tol).all()), float((err / tol).max())
     # the codes are exactly TR of the fp32 output the kernel wrote (tr_layer.py:96-99)
-    yq = oracle.tr(out.contiguous().cpu().numpy().reshape(1, -1, 1, 1), 0.05, 9, 1, 3)
-    exp = np.rint(yq.reshape(out.shape) / np.float32(0.05)).astype(np.int64)
+    yq = oracle.tr(out.contiguous().cpu().numpy().reshape(1, -1, 1, 1), sf, bw, 1, dt)
+    exp = np.rint(yq.reshape(out.shape) / np.float32(sf)).astype(np.int64)
     assert torch.equal(codes.cpu().long().permute(0, 3, 1, 2), torch.from_numpy(exp))
 
 
