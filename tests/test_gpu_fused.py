@@ -470,3 +470,46 @@ def test_fused_resnet_specialised_epilogues_bit_identical(monkeypatch):
         torch.cuda.synchronize()
         runs.append(logits.view(torch.int32).cpu())
     assert torch.equal(runs[0], runs[1])
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_act_encode_act_random_sweep(seed):
+    """Seeded random gate-and-encode passes (tq_act_encode_act): shapes (ragged channel
+    chunks, pad channels, non-square maps), activation (none / ReLU / ReLU6 / swish), gate,
+    code format and TR settings.  The fp32 output equals torch's composition on the GPU bit
+    for bit and the codes are the oracle's TR of (gate x) that value."""
+    rng = np.random.default_rng(6000 + seed)
+    n, c = int(rng.integers(1, 5)), int(rng.integers(1, 300))
+    h, w = int(rng.integers(1, 30)), int(rng.integers(1, 30))
+    cp = (c + 7) // 8 * 8 + 8 * int(rng.integers(0, 2))
+    act = [None, True, 6, "swish"][int(rng.integers(0, 4))]
+    gated = bool(rng.random() < 0.5)
+    fmt = torch.float16 if rng.random() < 0.5 else torch.int16
+    bw = int(rng.integers(4, 12))
+    dt = int(rng.integers(1, 5))
+    sf = float(10.0 ** rng.uniform(-3, 0))
+    torch.manual_seed(6000 + seed)
+    x = (torch.randn(n, c, h, w, device=DEV) * float(10.0 ** rng.uniform(-1, 1.5))).contiguous(
+        memory_format=torch.channels_last)
+    gate = torch.rand(n, c, device=DEV) if gated else None
+    codes = torch.full((n, h, w, cp), 77, dtype=fmt, device=DEV)
+    out = torch.empty_like(x)
+    tq_native.act_encode_act(x, sf, bw, dt, codes, act=act, gate=gate, out=out)
+    if act is None:
+        ref = x
+    elif act is True:
+        ref = torch.relu(x)
+    elif act == 6:
+        ref = torch.clamp(x, 0.0, 6.0)
+    else:
+        ref = x * torch.sigmoid(x)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.contiguous(
+        memory_format=torch.channels_last).view(torch.int32))
+    v = out.permute(0, 2, 3, 1).contiguous()
+    if gated:
+        v = v * gate[:, None, None, :]
+    exp = torch.from_numpy(oracle.tr(v.cpu().numpy(), sf, bw, 1, dt)) / np.float32(sf)
+    got = codes.float().cpu()
+    assert torch.equal(got[..., :c], exp.round())
+    assert (got[..., c:] == 0).all()
