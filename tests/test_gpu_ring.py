@@ -166,3 +166,25 @@ def test_ring_stream_k_bit_identical(cin, cout, hw, batch, grid, shape, monkeypa
                            kc_steps=kc[0], kc_chunk=kc[1])
             for g, e in zip(got, r):
                 assert (g is None and e is None) or torch.equal(g, e), (kc, form)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_ring_random_sweep(seed, monkeypatch):
+    """Seeded random ring-engine shapes (1-8 channel chunks, Cout a multiple of 4 up to 520,
+    maps 3-30, batch 1-8, persistent grids of 1 / 3 / 7 / default workgroups): outputs and
+    both code targets bit-identical to the VALU engine's."""
+    import numpy as np
+    rng = np.random.default_rng(7000 + seed)
+    cin = 64 * int(rng.integers(1, 9))
+    cout = 4 * int(rng.integers(2, 131))
+    hw = int(rng.integers(3, 31))
+    batch = int(rng.integers(1, 9))
+    conv, x, sc, sh, res = _case(cin, cout, hw, batch, seed=7000 + seed)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, cout, hw, cfg=0, sc=sc, sh=sh, res=res, codes_b=True,
+               fmt=torch.int16)
+    monkeypatch.setenv("TQ_RING_GRID", str(int(rng.choice([0, 1, 3, 7]))))
+    got = _run(cm, lay_m, cout, hw, cfg=RING, sc=sc, sh=sh, res=res, codes_b=True,
+               kc_steps=lay_m.kc_steps, kc_chunk=lay_m.kc_chunk)
+    assert torch.equal(got[0], ref[0])
+    assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2])
