@@ -151,3 +151,25 @@ def test_c64_bench_size_default_grid(batch, monkeypatch):
         got = _run(cm, lay_m, 56, cfg=C64, sc=sc, sh=sh, kc_steps=lay_m.kc_steps_nonneg, **kw)
         for g, r in zip(got, ref):
             assert (g is None and r is None) or torch.equal(g, r), form
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_c64_random_sweep(seed, monkeypatch):
+    """Seeded random layer-1 engine cases (maps 3-63 -- the widest halo the engine takes --,
+    batch 1-12, persistent grids of 1 / 2 / 3 / 37 / default workgroups, every epilogue form):
+    bit-identical to the VALU engine."""
+    import numpy as np
+    rng = np.random.default_rng(8000 + seed)
+    hw = int(rng.integers(3, 64))
+    batch = int(rng.integers(1, 13))
+    conv, x, sc, sh, res = _case(hw, batch, seed=8000 + seed)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    monkeypatch.setenv("TQ_C64_GRID", str(int(rng.choice([0, 1, 2, 3, 37]))))
+    form = sorted(FORMS)[int(rng.integers(0, len(FORMS)))]
+    kw = dict(FORMS[form])
+    if kw.pop("res", False):
+        kw["res"] = res
+    ref = _run(cv, lay_v, hw, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
+    got = _run(cm, lay_m, hw, cfg=C64, sc=sc, sh=sh, kc_steps=lay_m.kc_steps, **kw)
+    for g, r in zip(got, ref):
+        assert (g is None and r is None) or torch.equal(g, r), form
