@@ -107,3 +107,40 @@ def test_xp_default_switch(monkeypatch):
         got = _run(x, lay_m, 96, 14, cfg=0, sc=sc, sh=sh, fmt=torch.float16, act=6, out=True,
                    codes_b=False, kc_steps=lay_m.kc_steps)
         assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), v
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_xp_random_sweep(seed, monkeypatch):
+    """Seeded random expand-engine cases (input channels 8-96, Cout a multiple of 4 up to 600,
+    maps 3-30, batch 1-8, persistent grids, every epilogue form): bit-identical to the VALU
+    engine (swish: to the direct engine, the other MFMA engine with that epilogue)."""
+    import numpy as np
+    rng = np.random.default_rng(9000 + seed)
+    cin = 8 * int(rng.integers(1, 13))
+    cout = 4 * int(rng.integers(2, 151))
+    hw = int(rng.integers(3, 31))
+    batch = int(rng.integers(1, 9))
+    form = ["relu6_codes", "relu_codes", "swish_codes", "swish_out", "two_codes",
+            "signed"][int(rng.integers(0, 6))]
+    lay_v, lay_m = _layers(cin, cout, monkeypatch, seed=9000 + seed)
+    x = torch.relu(torch.randn(batch, cin, hw, hw, device=DEV)).contiguous(
+        memory_format=torch.channels_last)
+    sc = (torch.rand(cout, dtype=torch.float64, device=DEV) + 0.5) * 2e-4
+    sh = torch.randn(cout, dtype=torch.float64, device=DEV) * 0.1
+    kw = dict(relu6_codes=dict(act=6, out=False, codes_b=False),
+              relu_codes=dict(act=True, out=False, codes_b=False),
+              swish_codes=dict(act="swish", out=False, codes_b=False),
+              swish_out=dict(act="swish", out=True, codes_b=False),
+              two_codes=dict(act=True, out=True, codes_b=True),
+              signed=dict(act=False, out=True, codes_b=False))[form]
+    if form.startswith("swish"):
+        ref = _run(x, lay_m, cout, hw, cfg=DIRECT, sc=sc, sh=sh, fmt=torch.float16,
+                   kc_steps=lay_m.kc_steps, **kw)
+    else:
+        ref = _run(x, lay_v, cout, hw, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
+    monkeypatch.setenv("TQ_XP_GRID", str(int(rng.choice([0, 1, 3]))))
+    monkeypatch.setenv("TQ_XP_GROUPS", "8")
+    got = _run(x, lay_m, cout, hw, cfg=XP, sc=sc, sh=sh, fmt=torch.float16,
+               kc_steps=lay_m.kc_steps, **kw)
+    for g, r in zip(got, ref):
+        assert (g is None and r is None) or torch.equal(g, r), form
