@@ -40,7 +40,10 @@ import util  # noqa: E402
 
 METRIC = "term-pair MACs/sec + images/sec, ResNet-18 TQ g=8 at 1/2/4/8 MI355X"
 WB, G, K, DB, DT = 9, 8, 12, 9, 3
-STEM_NAMES = {"fused": "split-fp16 near-fp32 (fused stem kernel)",
+STEM_NAMES = {"fused": "fp32-exact codes (fused stem kernel: split-fp16 MFMA conv + exact fp64 "
+                       "recompute of every output within the split's error bound of a "
+                       "rounding midpoint)",
+              "split": "split-fp16 near-fp32 (fused stem kernel, no fix-up)",
               "fp32": "torch fp32 conv (MIOpen) + BN/ReLU/max-pool/codes kernel"}
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 HBM_BYTES_PER_IMAGE = 15026432   # algorithmic bytes of the TR path per image
@@ -81,9 +84,11 @@ def parse(argv=None):
     ap.add_argument("--no-d4", action="store_true",
                     help="skip the d4 key (BASELINE configs[2]/[3]: LSTM-650, fused "
                          "MobileNet-V2 / EfficientNet-b0; rank 0 at N=1 only)")
-    ap.add_argument("--stem", choices=("fused", "fp32"), default="fused",
-                    help="fused: the stem conv in the fused stem kernel (split-fp16 near-fp32); "
-                         "fp32: torch's fp32 conv + the BN/ReLU/max-pool/codes kernel")
+    ap.add_argument("--stem", choices=("fused", "split", "fp32"), default="fused",
+                    help="fused: the fused stem kernel + its exact fix-up (codes of the "
+                         "correctly rounded fp32 conv); split: the fused stem kernel alone "
+                         "(split-fp16 near-fp32); fp32: torch's fp32 conv + the "
+                         "BN/ReLU/max-pool/codes kernel")
     ap.add_argument("--no-stem-leg", action="store_true",
                     help="skip the second timed pass with the other stem (N=1 only)")
     ap.add_argument("--unfused", action="store_true",
@@ -164,11 +169,14 @@ def spawn_ranks(argv, n, dry, timeout_s=None, poll_s=0.2):
 
 
 def check_world(world, local):
-    """A rank's own check that its GPU exists (spawn_ranks leaves the count to the ranks)."""
+    """A rank's own check that its GPU exists (spawn_ranks leaves the count to the ranks).
+    Per node: the ranks of this node (LOCAL_WORLD_SIZE, torchrun's; WORLD_SIZE when unset)
+    must fit its visible GPUs, so a multi-node torchrun (WORLD_SIZE > GPUs per node) passes."""
     have = torch.cuda.device_count()
-    if local >= have or world > have:
-        print("bench.py: world size %d (local rank %d) but only %d GPU(s) visible" %
-              (world, local, have), file=sys.stderr)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if local >= have or local_world > have:
+        print("bench.py: %d rank(s) on this node (local rank %d, world size %d) but only %d "
+              "GPU(s) visible" % (local_world, local, world, have), file=sys.stderr)
         return False
     return True
 
@@ -348,7 +356,12 @@ def cpu_python_baselines(oracle, nq=200000, nx=1 << 16):
     return {"c1_hese_values_per_s": nq / t_hese, "c2_tr_elements_per_s": nx / t_tr,
             "cores": 1, "kind": "port", "c2_matches_c_restatement": ok,
             "sample": "C1: %d random q in [-511, 511] (seed 0), oracle.hese_py; C2: %d relu(N(0,1)) "
-                      "fp32, g=8 k=12 sf=0.05 db=%d, oracle.tr_py" % (nq, nx, DB)}
+                      "fp32, g=8 k=12 sf=0.05 db=%d, oracle.tr_py" % (nq, nx, DB),
+            # C1 times the restatement; the reference's own encoder (bit_utils.hese,
+            # bit_utils.py:10-44) cannot travel to the GPU box and is timed in the build
+            # container on the same sample by tools/ref/time_ref_hese.py
+            "c1_is": "restatement (oracle.hese_py), not the reference's bit_utils.hese",
+            "c1_reference_encoder": "profiles/r06_ref_hese_cpu.txt"}
 
 
 def cpu_tr_op_baseline(oracle, n=1 << 24):
@@ -542,7 +555,7 @@ def main(argv=None):
         # price of the fused split-fp16 stem's precision choice, reported beside the headline
         stem_leg = None
         if world == 1 and not args.unfused and not args.no_stem_leg:
-            other = "fp32" if args.stem == "fused" else "fused"
+            other = "fused" if args.stem == "fp32" else "fp32"
             el2, launch2, _ = timed_steps(tq_fuse.FusedResNet(qmodel, stem=other))
             stem_leg = {"stem": STEM_NAMES[other], "images_per_s": args.batch * args.steps / el2,
                         "ms_per_step": el2 / args.steps * 1e3, "launch": launch2,
@@ -640,7 +653,10 @@ def main(argv=None):
             roof_tr = {
                 "kernel": "stem_conv_pool_kernel (ResNet stem conv 7x7/2 in near-fp32 arithmetic "
                           "on split-fp16 v_mfma_f32_16x16x32_f16 + BN/ReLU/max-pool + first "
-                          "activation TR -> fp16 codes)",
+                          "activation TR -> fp16 codes)" + (
+                              " + stem_fixup_kernel (exact fp64 recompute of the listed "
+                              "near-midpoint outputs; time included)"
+                              if args.stem == "fused" else ""),
                 "bound": "mfma",
                 # what the matrix cores execute: 3 fp16 split products per fp32 MAC, against
                 # the dense fp16 MFMA peak
@@ -700,7 +716,7 @@ def main(argv=None):
                        # the stem conv (not a TR layer; fp32 torch in the reference) runs in
                        # the fused stem kernel as a split-fp16 near-fp32 conv,
                        # or (--stem fp32) as torch's fp32 conv
-                       "stem": STEM_NAMES["fused" if enc_name == "stem_conv_pool" else "fp32"]},
+                       "stem": STEM_NAMES[args.stem if enc_name == "stem_conv_pool" else "fp32"]},
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,
             "roofline": roof,
@@ -708,7 +724,7 @@ def main(argv=None):
             "accuracy_counters": acc_counters,
         }
         if stem_leg is not None:
-            result["stem_fp32" if args.stem == "fused" else "stem_fused"] = stem_leg
+            result["stem_fused" if args.stem == "fp32" else "stem_fp32"] = stem_leg
         if world == 1 and not args.no_d1:
             result["d1_tr_op"] = d1_tr_op(dev)
         if world == 1 and not args.no_d4:

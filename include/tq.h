@@ -362,6 +362,18 @@ int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, i
  *            2sx+sub_c-1), zero where a tap index is -1 (term-quantization_amd/tq_ops.py
  *            pack_stem_weight)
  *   out      fp32 [n][h/4][w/4][64] (ho = h/4, wo = w/4)
+ * Exact fix-up (w64, wbound, workspace all non-NULL; all NULL = the split conv's result
+ * stands): the split conv of output channel c is within wbound[c] * M of the exact sum (M
+ * the max |x| of the input rows the kernel staged for it).  Every output whose quotient
+ * out / sf lies within that error (through BN) of a rounding midpoint is listed in the
+ * workspace and recomputed by a second kernel on the same stream from the fp64 weights --
+ * exact products, fp64 sum, one rounding to fp32 -- so every code equals the code of the
+ * correctly rounded fp32 conv followed by the same BN / ReLU / max-pool.
+ *   w64      fp64 [64][7][7][3] conv weights (kernel row, column, input channel)
+ *   wbound   fp32 [64], >= the split conv's relative error bound times sum |w[c]|
+ *            (tq_ops.pack_stem_exact)
+ *   workspace  >= tq_stem_workspace_bytes(n, h, w) bytes, 16-byte aligned; needs
+ *            n * ho * wo < 2^24
  * TQ_ERR_UNSUPPORTED when the image is too wide for one LDS tile (w/4 > 84).
  */
 int tq_stem_conv_pool_encode(const float *x, int64_t n, int64_t h, int64_t w,
@@ -369,7 +381,13 @@ int tq_stem_conv_pool_encode(const float *x, int64_t n, int64_t h, int64_t w,
                              float *out, int64_t ho, int64_t wo, void *codes_a, int64_t cp_a,
                              float sf_a, int32_t bits_a, int32_t terms_a, int32_t fmt_a,
                              void *codes_b, int64_t cp_b, float sf_b, int32_t bits_b,
-                             int32_t terms_b, int32_t fmt_b, void *stream);
+                             int32_t terms_b, int32_t fmt_b, const double *w64,
+                             const float *wbound, void *workspace, int64_t workspace_bytes,
+                             void *stream);
+
+/* Workspace bytes tq_stem_conv_pool_encode's exact fix-up needs for an n x 3 x h x w batch
+ * (-1 for invalid sizes). */
+int64_t tq_stem_workspace_bytes(int64_t n, int64_t h, int64_t w);
 
 /*
  * Batched activation-scale calibration, replacing the 2048-launch loop of

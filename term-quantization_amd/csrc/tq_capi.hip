@@ -599,12 +599,21 @@ int tq_bn_relu_maxpool_encode(const float* x, int64_t n, int64_t h, int64_t w, i
                     "bn_relu_maxpool launch");
 }
 
+int64_t tq_stem_workspace_bytes(int64_t n, int64_t h, int64_t w) {
+  if (n < 0 || h < 4 || w < 4 || h > (1 << 20) || w > (1 << 20)) return -1;
+  // per-workgroup counts, then one entry per (pool pixel, channel quad) of every tile (tiles
+  // of up to four pool rows: at most 3 rows past Ho)
+  return tq::kStemFixCountsBytes + n * (h / 4 + 3) * (w / 4) * 16 * 4;
+}
+
 int tq_stem_conv_pool_encode(const float* x, int64_t n, int64_t h, int64_t w,
                              const uint16_t* w_split, const float* scale, const float* shift,
                              float* out, int64_t ho, int64_t wo, void* codes_a, int64_t cp_a,
                              float sf_a, int32_t bits_a, int32_t terms_a, int32_t fmt_a,
                              void* codes_b, int64_t cp_b, float sf_b, int32_t bits_b,
-                             int32_t terms_b, int32_t fmt_b, void* stream) {
+                             int32_t terms_b, int32_t fmt_b, const double* w64,
+                             const float* wbound, void* workspace, int64_t workspace_bytes,
+                             void* stream) {
   if (n < 0 || h < 4 || w < 4 || h % 4 || w % 4 || ho != h / 4 || wo != w / 4 ||
       h > (1 << 20) || w > (1 << 20))
     return fail(TQ_ERR_INVALID_ARGUMENT, "stem_conv_pool: needs H, W % 4 == 0 and Ho = H/4, "
@@ -650,6 +659,23 @@ int tq_stem_conv_pool_encode(const float* x, int64_t n, int64_t h, int64_t w,
   // the pooled outputs are ReLU'd: the epilogue code tables apply
   a.lut_a = lut_entries(codes_a != nullptr, true, a.inv_a, a.maxv_a);
   a.lut_b = lut_entries(codes_b != nullptr, true, a.inv_b, a.maxv_b);
+  if (w64 || wbound || workspace) {  // the exact fix-up: all three or none
+    if (!w64 || !wbound || !workspace || (uintptr_t)w64 % 8 || (uintptr_t)wbound % 4 ||
+        (uintptr_t)workspace % 16)
+      return fail(TQ_ERR_INVALID_ARGUMENT,
+                  "stem_conv_pool: exact fix-up needs w64, wbound and workspace (aligned)");
+    if (workspace_bytes < tq_stem_workspace_bytes(n, h, w))
+      return fail(TQ_ERR_INVALID_ARGUMENT, "stem_conv_pool: workspace too small "
+                                           "(tq_stem_workspace_bytes)");
+    // list entries are ((pixel * 16 + quad) << 4) | mask in 32 bits
+    if (n * ho * wo >= (int64_t)1 << 24)
+      return fail(TQ_ERR_UNSUPPORTED, "stem_conv_pool: exact fix-up needs n*ho*wo < 2^24");
+    a.w64 = w64;
+    a.wbound = wbound;
+    a.fix_counts = static_cast<uint32_t*>(workspace);
+    a.fix_list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) +
+                                             tq::kStemFixCountsBytes);
+  }
   const hipError_t e = tq::launch_stem_conv_pool(a, (hipStream_t)stream);
   if (e == hipErrorInvalidConfiguration)
     return fail(TQ_ERR_UNSUPPORTED, "stem_conv_pool: image too wide for the LDS tile");

@@ -138,7 +138,19 @@ struct PoolArgs {
   // fused stem (tq_stem_conv.hip): x is the [N][H][W][3] input image, H/W its size, and
   // wsplit the conv weights * 2^10 as two fp16 splits [2][64][192] (s2d K order)
   const uint16_t* wsplit;
+  // fused stem, exact fix-up (nullptr fix_list: the split-fp16 result stands): w64 the conv
+  // weights in fp64 [64][7][7][3] (kernel row, column, channel: the image's NHWC order),
+  // wbound[c] >= err_rel * sum |w[c]| (the split conv's error per unit of the input tile's
+  // max |x|), fix_list / fix_counts the per-workgroup lists of near-midpoint outputs
+  const double* w64;
+  const float* wbound;
+  uint32_t* fix_list;
+  uint32_t* fix_counts;
 };
+
+// fused stem exact fix-up workspace: per-workgroup entry counts (stem grids <= 1024), then
+// the entry lists
+constexpr int64_t kStemFixCountsBytes = 4096;
 
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream);

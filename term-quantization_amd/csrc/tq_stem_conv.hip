@@ -49,7 +49,7 @@
 #include "tq_launch.h"
 
 #ifndef STEM_AB
-#define STEM_AB 0  // timing-only ablation builds (tools/variant1.sh); 0 = the product kernel
+#define STEM_AB 0  // timing-only ablation builds (tools/ab/variant1.sh); 0 = the product kernel
 #endif
 #ifndef STEM_CARRY
 #define STEM_CARRY 1  // 1: a tile's first conv row carried from the tile above (one strip per wave)
@@ -83,7 +83,7 @@ constexpr int kStemWRow = 208;  // LDS weight row (bf16): 416 B makes the A read
 constexpr int kStemWBytes = 2 * 64 * kStemWRow * 2;
 constexpr int kStemWExp = 10;   // weights are split as w * 2^10 (tq_ops.pack_stem_weight)
 constexpr int kStemXMag = 14;   // a tile's inputs are scaled to max |x| < 2^14
-constexpr int kStemDynLds = 160 * 1024 - 256;  // the rest of the CU's LDS: static tile_max
+constexpr int kStemDynLds = 160 * 1024 - 1024;  // the rest of the CU's LDS: static arrays
 
 // __shfl_down(v, D, 16) as a DPP row shift (no LDS permute): lane i of each 16-lane row
 // reads lane i + D; lanes whose source is past the row end keep their own value.
@@ -100,6 +100,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
                                                                          int nb, int tiles) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds_raw[];
   __shared__ uint32_t tile_max[2];  // max |x| (fp32 bits) of a tile's rows, by tile parity
+  __shared__ uint32_t fix_n;        // near-midpoint outputs this workgroup listed (fix-up)
+  __shared__ float fix_ew[2][64];   // per side and channel: quotient error per unit max |x|
   uint16_t* ws = reinterpret_cast<uint16_t*>(lds_raw);
   float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(lds_raw) + kStemWBytes);
   // per-wave pool staging: 7 pixels x 64 channels fp32 behind the input rows
@@ -139,6 +141,17 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   for (int i = 0; i < 4; ++i) {
     bsc[i] = fabsf(a.scale[4 * i16 + i]);
     bsh[i] = a.shift[4 * i16 + i];
+  }
+  // Exact fix-up (a.fix_list): the split conv of channel c is within wbound[c] * M of the
+  // exact sum, M the max |x| of the input rows it read, so an output whose quotient y / sf
+  // lies within M * ew[c] (+ two ulps of slack for the BN fma and the quotient's rounding) of
+  // a rounding midpoint is the only kind whose code can differ from the exact conv's; those
+  // are listed for stem_fixup_kernel, which recomputes them exactly.
+  const bool fix = a.fix_list != nullptr;
+  if (fix && tid < 128) {  // visible after the first barrier
+    const int c = tid & 63;
+    const float wb = a.wbound[c] * fabsf(a.scale[c]) * 1.0009765625f;
+    fix_ew[tid >> 6][c] = wb * (float)(tid < 64 ? a.inv_a : a.inv_b);
   }
 
   // Input staging, software-pipelined across tiles: the next tile's rows are loaded into
@@ -204,6 +217,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   if (tid == 0) {
     tile_max[0] = 0u;
     tile_max[1] = 0u;
+    fix_n = 0u;
   }
   // Each workgroup walks a contiguous run of tiles (top to bottom through its images): the
   // 2 TP + 4 s2d rows of a tile overlap the previous tile's by 4, and those halo rows were
@@ -212,6 +226,9 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
   if (t_begin < t_end) prefetch(t_begin);
+  // this workgroup's segment of the fix-up list: one entry at most per (pool pixel, 4-channel
+  // quad) of its tiles
+  uint32_t* fix_seg = fix ? a.fix_list + (int64_t)t_begin * TP * a.Wo * 16 : nullptr;
   __syncthreads();
 
   // fp16 operands need a range: each tile's inputs are scaled by 2^kx so that max |x| <
@@ -224,6 +241,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   constexpr bool one = ONE;
   f32x4 carry[4];
   int prev_tile = -2, prev_kx = 0;
+  float prev_tm = 0.0f;
   for (int tile = t_begin; tile < t_end; ++tile, ++it) {
 #if STEM_TRACE
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
@@ -257,6 +275,11 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       kx = kStemXMag - e;
     }
     const int kback = -(kx + kStemWExp);
+    // the max |x| behind this tile's conv rows (a carried row was read in the previous tile)
+    const float cur_tm = __uint_as_float(mbits);
+    const bool carried = ONE && STEM_CARRY && py0 != 0 && tile == prev_tile + 1 &&
+                         n == prev_tile / tpi && kx == prev_kx;
+    const float tm = carried ? fmaxf(cur_tm, prev_tm) : cur_tm;
     if (STEM_AB != 3) commit(kx);  // (3: timing only, no input staging)
     if (tid == 0) tile_max[(it + 1) & 1] = 0u;
     __syncthreads();  // B
@@ -401,7 +424,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int f = lane + 64 * h;  // quad: pixel f / 16, channels 4 (f % 16) .. +3
-          if (f >= 16 * npx) continue;
+          uint32_t ent = 0u;             // fix-up list entry of this quad (0: none)
+          if (f < 16 * npx) {
           const int co = 4 * (f & 15);
           const int64_t p = p0 + (f >> 4);
           const f32x4 v4 = *reinterpret_cast<const f32x4*>(pb + 4 * f);
@@ -428,6 +452,17 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             const int fmt = side ? a.fmt_b : a.fmt_a;
             uint32_t v[4];
             const uint16_t* lut = side ? lut_b : lut_a;
+            if (fix) {  // near-midpoint quotients, listed for the exact fix-up
+              uint32_t fm = 0u;
+              const f32x4 ew = *reinterpret_cast<const f32x4*>(&fix_ew[side][co]);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float r = fminf(quotient_f32(yv[i], inv), maxv);
+                if (fabsf(__builtin_amdgcn_fractf(r) - 0.5f) <= fmaf(tm, ew[i], 0x1p-12f))
+                  fm |= 1u << i;
+              }
+              if (fm) ent = ((uint32_t)(p * 16 + (f & 15)) << 4) | (ent & 15u) | fm;
+            }
             if (lut) {  // the fast path's codes from the LDS table
 #pragma unroll
               for (int i = 0; i < 4; ++i) v[i] = lut[relu_q(yv[i], inv, maxv)];
@@ -446,6 +481,20 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             } else {
               *reinterpret_cast<int2*>(codes + p * cp + co) =
                   make_int2((int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)));
+            }
+          }
+          }
+          if (fix) {  // append the wave's entries to the workgroup's segment
+            const uint64_t bal = __ballot(ent != 0u);
+            if (bal) {
+              uint32_t base = 0u;
+              if (lane == 0) base = atomicAdd(&fix_n, (uint32_t)__popcll(bal));
+              base = __builtin_amdgcn_readfirstlane(base);
+              if (ent) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                fix_seg[base + rank] = ent;
+              }
             }
           }
         }
@@ -523,6 +572,91 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #endif
     prev_tile = tile;
     prev_kx = kx;
+    prev_tm = cur_tm;
+  }
+  if (fix) {
+    __syncthreads();
+    if (tid == 0) a.fix_counts[blockIdx.x] = fix_n;
+  }
+}
+
+// Exact fix-up of the listed outputs (one launch after the stem, same stream).  Each entry
+// names a pool pixel p and a 4-bit mask of channels in quad cq; for each such channel the
+// nine conv outputs of its pool window are recomputed exactly -- fp32 x times fp32 w is exact
+// in fp64 and a 147-term fp64 sum is within 2^-46 of its magnitude sum, then one rounding to
+// fp32 -- and the pooled value goes through the same BN fma, ReLU and code path as the
+// stem's epilogue.  A wave holds 7 entries x 9 window positions (lane = 9 slot + j), the
+// window max gathered by lane shuffles.  Grid: (stem workgroups, slices); block (g, s) walks
+// the entries of stem workgroup g's segment.
+constexpr int kFixThreads = 256;
+constexpr int kFixSlices = 8;
+
+__global__ __launch_bounds__(kFixThreads) void stem_fixup_kernel(PoolArgs a, int tp,
+                                                                 int tiles) {
+  const int g = blockIdx.x;
+  const int t_begin = (int)((int64_t)g * tiles / gridDim.x);
+  const uint32_t* seg = a.fix_list + (int64_t)t_begin * tp * a.Wo * 16;
+  const int cnt = (int)a.fix_counts[g];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int slot = lane / 9;
+  const int j = lane - 9 * slot;
+  const int Hc = a.H / 2, Wc = a.W / 2;
+  const int stride = gridDim.y * (kFixThreads / 64) * 7;
+  for (int i0 = (blockIdx.y * (kFixThreads / 64) + wave) * 7; i0 < cnt; i0 += stride) {
+    const int i = i0 + slot;
+    const bool act = slot < 7 && i < cnt;
+    const uint32_t ent = act ? seg[i] : 0u;
+    uint32_t m = ent & 15u;
+    const uint32_t pq = ent >> 4;
+    const int64_t p = pq >> 4;
+    const int cq = (int)(pq & 15u);
+    const int px = (int)(p % a.Wo);
+    const int64_t t = p / a.Wo;
+    const int py = (int)(t % a.Ho);
+    const int64_t n = t / a.Ho;
+    const int oy = 2 * py - 1 + j / 3;
+    const int ox = 2 * px - 1 + j % 3;
+    const bool valid = act && oy >= 0 && oy < Hc && ox >= 0 && ox < Wc;
+    while (__ballot(m != 0u)) {  // the wave's entries, one channel each round
+      const bool has = m != 0u;
+      const int c = 4 * cq + (has ? __builtin_ctz(m) : 0);
+      m &= m - 1u;
+      float v = -__builtin_inff();
+      if (has && valid) {
+        const double* wc = a.w64 + c * 147;
+        double acc = 0.0;
+        for (int ky = 0; ky < 7; ++ky) {
+          const int iy = 2 * oy - 3 + ky;
+          if (iy < 0 || iy >= a.H) continue;
+          const float* xr = a.x + ((n * a.H + iy) * a.W) * 3;
+#pragma unroll
+          for (int kx = 0; kx < 7; ++kx) {
+            const int ix = 2 * ox - 3 + kx;
+            if (ix < 0 || ix >= a.W) continue;
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci)
+              acc = fma((double)xr[ix * 3 + ci], wc[(ky * 7 + kx) * 3 + ci], acc);
+          }
+        }
+        v = (float)(__builtin_signbit(a.scale[c]) ? -acc : acc);
+      }
+      // window max on lane 9 slot (the shuffles read lanes of the same slot; lane 63's
+      // reads wrap and are unused)
+      float vm = v;
+#pragma unroll
+      for (int jj = 1; jj < 9; ++jj) vm = fmaxf(vm, __shfl(v, lane + jj));
+      if (has && j == 0) {
+        const float y = fmaxf(fmaf(vm, fabsf(a.scale[c]), a.shift[c]), 0.0f);
+        a.out[p * 64 + c] = y;
+        if (a.codes_a)
+          a.codes_a[p * a.cp_a + c] =
+              (int16_t)code_bits(tr_value_g1_inv(y, a.inv_a, a.maxv_a, a.k_a), a.fmt_a);
+        if (a.codes_b)
+          a.codes_b[p * a.cp_b + c] =
+              (int16_t)code_bits(tr_value_g1_inv(y, a.inv_b, a.maxv_b, a.k_b), a.fmt_b);
+      }
+    }
   }
 }
 
@@ -555,8 +689,14 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
     cus = 256;
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return hipSuccess;
+  if (a.fix_list && grid * 4 > kStemFixCountsBytes) return hipErrorInvalidValue;
   stem_conv_pool_kernel<TP, QMAX, ONE><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(
       b, sc, nb, tiles);
+  if (a.fix_list) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    stem_fixup_kernel<<<dim3(grid, kFixSlices), kFixThreads, 0, stream>>>(b, TP, tiles);
+  }
   return hipGetLastError();
 }
 

@@ -39,11 +39,15 @@
 //     partner's matrix work on every SIMD.  Only waves 0-3 issue the ring DMA, so a late
 //     wave's residual registers (loaded before its MFMAs, consumed after the next barrier)
 //     never wait behind a DMA in its own vmcnt queue;
-//   * residual loads and all epilogue stores are buffer instructions with per-lane offsets
-//     (a pixel block past the tensor gets an offset past the buffer: loads read 0, stores are
-//     dropped), so no store is skipped by a branch and the vmcnt count a wave waits with
-//     before the barrier (its DMA is older than exactly its epilogue's stores) is a
-//     compile-time constant.
+//   * residual loads and all epilogue stores are buffer instructions with per-lane offsets,
+//     so no store is skipped by a branch and the vmcnt count a wave waits with before the
+//     barrier (its DMA is older than exactly its epilogue's stores) is a compile-time
+//     constant.  A pixel block past the tensor would get an offset past the buffer (loads
+//     read 0, stores dropped), but under conv_c64_eligible (P % 32 == 0) no wave owns such a
+//     block: a wave whose block starts at or past its workgroup's range end returns before
+//     its residual loads and epilogue (the late epilogue is gated the same way), so those
+//     offsets are defense in depth only (tests/test_gpu_c64.py checks a guard tail behind
+//     every output buffer).
 //
 //   LDS = weights [64][73 x 16 B] | ring [640][128 B] | zero pixel (128 B) | code tables
 #include <stdlib.h>
@@ -56,7 +60,7 @@
 #include "tq_mfma.h"
 
 #ifndef C64_AB
-#define C64_AB 0  // timing-only ablation builds (tools/variant1.sh); 0 = the product kernel
+#define C64_AB 0  // timing-only ablation builds (tools/ab/variant1.sh); 0 = the product kernel
 #endif
 #ifndef C64_PF
 #define C64_PF 2  // substeps of fragment prefetch (2: conv1 77 -> 73 us; residual forms equal)

@@ -32,14 +32,14 @@
 #include "tq_mfma.h"
 
 #ifndef TQ_ABLATE
-#define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
+#define TQ_ABLATE 0  // timing-only ablation builds (tools/ab/ablate.sh); 0 = the product kernel
 #endif
 
 #ifndef TQ_DIR_ASM_DMA
 #define TQ_DIR_ASM_DMA 1  // 0: the weight DMA through the builtin (timing variants only)
 #endif
 #ifndef TQ_PHASE_TRACE
-#define TQ_PHASE_TRACE 0  // timing-only builds (tools/variant.sh): per-workgroup phase stamps
+#define TQ_PHASE_TRACE 0  // timing-only builds (tools/ab/variant.sh): per-workgroup phase stamps
 #endif
 
 namespace tq {

@@ -512,6 +512,10 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   a.m_slow = ms ? atoi(ms) : 0;
   const bool pipe_ok = a.Cp % kKStep == 0 && a.KH * a.KW <= 64;
   int cfg = a.config > 0 ? a.config - 1 : -1;
+  // TQ_CONFIG_STRICT=1 (tests): a requested engine config that cannot take the conv is an
+  // error instead of a quiet fall-back to the default engine (read per launch)
+  const char* strict_env = getenv("TQ_CONFIG_STRICT");
+  const bool strict = strict_env && atoi(strict_env) == 1;
   static const char* ab = getenv("TQ_AB");
   a.ab = ab ? atoi(ab) : 0;
   static const char* dir = getenv("TQ_DIRECT");  // A/B override (tools only): 0 off, 1/2 MB
@@ -523,14 +527,18 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   const char* pw = getenv("TQ_PW");  // read per launch: tests switch it
   if ((cfg == 11 || (cfg < 0 && pw && atoi(pw) == 1)) && conv_pw_eligible(a, out_nhwc))
     return launch_conv2d_pw(a, stream);
+  if (cfg == 11 && strict) return hipErrorInvalidValue;
   // expand engine: config 14, and the default for the 1x1 convs it takes (MobileNet-V2 /
-  // EfficientNet-b0 expand convs: 112^2 x 16 -> 96 534 -> 408 us, tools/gpu_expand_probe.sh);
+  // EfficientNet-b0 expand convs: 112^2 x 16 -> 96 534 -> 408 us, tools/ab/gpu_expand_probe.sh);
   // TQ_XP=0 / 1 forces it off / on (read per launch: tests switch it)
   const char* xp = getenv("TQ_XP");
   const bool xp_on = xp ? atoi(xp) == 1 : true;
   if ((cfg == 13 || (cfg < 0 && xp_on)) && conv_xp_eligible(a, out_nhwc))
     return launch_conv2d_xp(a, stream);
-  if (cfg == 13) cfg = -1;
+  if (cfg == 13) {
+    if (strict) return hipErrorInvalidValue;
+    cfg = -1;
+  }
   if (a.relu == kActSwish) {  // the swish epilogue exists on the direct engine only
     if (!conv_direct_eligible(a, out_nhwc)) return hipErrorInvalidValue;
     return launch_conv2d_direct(a, 1, stream);
@@ -546,7 +554,10 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   const bool ring_on = ring ? atoi(ring) == 1 : a.Cout >= 128;
   if ((cfg == 12 || (cfg < 0 && ring_on)) && conv_ring_eligible(a, out_nhwc))
     return launch_conv2d_ring(a, stream);
-  if (cfg == 12) cfg = -1;
+  if (cfg == 12) {
+    if (strict) return hipErrorInvalidValue;
+    cfg = -1;
+  }
   // Cout-64 pixel-ring engine: config 15, and the default for the layer-1 convs it takes
   // (TQ_C64=0 / 1 forces it off / on; read per launch: tests switch it)
   // (its epilogues are all specialised ReLU + table forms: TQ_EPI_FAST=0, the generic-epilogue
@@ -556,11 +567,17 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   const bool c64_on = c64 ? atoi(c64) == 1 : !(epi_fast && atoi(epi_fast) == 0);
   if ((cfg == 14 || (cfg < 0 && c64_on)) && conv_c64_eligible(a, out_nhwc))
     return launch_conv2d_c64(a, stream);
-  if (cfg == 14) cfg = -1;
+  if (cfg == 14) {
+    if (strict) return hipErrorInvalidValue;
+    cfg = -1;
+  }
   static const char* strip = getenv("TQ_STRIP");  // A/B override (tools only): 0 off
   if (cfg == 10 || (cfg < 0 && !(strip && atoi(strip) == 0))) {
     if (conv_strip_eligible(a, out_nhwc)) return launch_conv2d_strip(a, stream);
-    if (cfg == 10) cfg = -1;
+    if (cfg == 10) {
+      if (strict) return hipErrorInvalidValue;
+      cfg = -1;
+    }
   }
   // measured (tools/layer_times.py, ResNet-18 batch 256): the direct engine wins where the
   // fused epilogue dominates -- Cout <= 128 (layer1/2) and 1x1 convs
@@ -570,6 +587,7 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
   if (cfg >= 8) {
     if (conv_direct_eligible(a, out_nhwc))
       return launch_conv2d_direct(a, cfg == 8 ? 2 : 1, stream);
+    if (strict && a.config > 0) return hipErrorInvalidValue;
     cfg = -1;
   }
   if (cfg >= 6 || cfg < 0) {
@@ -577,6 +595,7 @@ hipError_t launch_conv2d_mfma(const ConvArgs& a_in, int out_nhwc, hipStream_t st
       const int mb = cfg == 6 ? 2 : cfg == 7 ? 1 : (a.Cout <= 64 ? 1 : 2);
       return launch_conv2d_patch(a, mb, stream);
     }
+    if (strict && cfg >= 6) return hipErrorInvalidValue;
     cfg = -1;
   }
   // measured (tools/microbench.py --sweep): 64 x 512 (8 waves) for Cout <= 64, else 128 x 256

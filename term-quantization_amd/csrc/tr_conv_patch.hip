@@ -27,10 +27,10 @@
 #include "tq_mfma.h"
 
 #ifndef TQ_ABLATE
-#define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
+#define TQ_ABLATE 0  // timing-only ablation builds (tools/ab/ablate.sh); 0 = the product kernel
 #endif
 #ifndef TQ_PATCH_SCHED
-#define TQ_PATCH_SCHED 1  // 0: the round-2 schedule (timing variants only, tools/variant.sh)
+#define TQ_PATCH_SCHED 1  // 0: the round-2 schedule (timing variants only, tools/ab/variant.sh)
 #endif
 
 namespace tq {

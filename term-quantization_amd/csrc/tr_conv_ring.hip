@@ -45,7 +45,7 @@
 #include "tq_mfma.h"
 
 #ifndef RING_AB
-#define RING_AB 0  // timing-only ablation builds (tools/variant.sh); 0 = the product kernel
+#define RING_AB 0  // timing-only ablation builds (tools/ab/variant.sh); 0 = the product kernel
 #endif
 #ifndef RING_DMA_LATE
 #define RING_DMA_LATE 0  // 1: a step's DMA issued after its first substep (A/B builds)

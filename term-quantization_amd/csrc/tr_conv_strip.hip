@@ -38,7 +38,7 @@
 #include "tq_mfma.h"
 
 #ifndef TQ_ABLATE
-#define TQ_ABLATE 0  // timing-only ablation builds (tools/ablate.sh); 0 = the product kernel
+#define TQ_ABLATE 0  // timing-only ablation builds (tools/ab/ablate.sh); 0 = the product kernel
 #endif
 
 namespace tq {

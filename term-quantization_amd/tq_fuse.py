@@ -183,14 +183,17 @@ class FusedResNet(nn.Module):
     """Inference executor over a converted + calibrated torchvision-style ResNet.
 
     ``stem="fused"`` (default) runs conv1 + bn1 + relu + maxpool + the first codes as one
-    kernel whose conv is split-fp16 near-fp32; ``stem="fp32"`` keeps torch's fp32
-    conv1 (MIOpen's true fp32: gfx950 has no TF32 / xf32) and runs only BN + ReLU + max-pool +
-    codes in one kernel -- the reference's arithmetic for the stem conv (bench.py --stem)."""
+    kernel whose conv is split-fp16 on the matrix cores, followed by the exact fix-up of every
+    output whose code the split's error could change: the codes are those of the
+    correctly rounded fp32 conv.  ``stem="split"`` skips the fix-up (the split-fp16 result, an
+    A/B and test mode); ``stem="fp32"`` keeps torch's fp32 conv1 (MIOpen's true fp32: gfx950
+    has no TF32 / xf32) and runs only BN + ReLU + max-pool + codes in one kernel -- the
+    reference's arithmetic for the stem conv (bench.py --stem)."""
 
     def __init__(self, qmodel, stem="fused"):
         super(FusedResNet, self).__init__()
-        if stem not in ("fused", "fp32"):
-            raise ValueError("stem must be 'fused' or 'fp32'")
+        if stem not in ("fused", "split", "fp32"):
+            raise ValueError("stem must be 'fused', 'split' or 'fp32'")
         self.qmodel = qmodel
         self.blocks = []
         for layer in (qmodel.layer1, qmodel.layer2, qmodel.layer3, qmodel.layer4):
@@ -209,7 +212,8 @@ class FusedResNet(nn.Module):
         # torchvision shape: conv 7x7/2 pad 3, 3 -> 64, no bias; pool 3x3/2 pad 1
         c1 = qmodel.conv1
         self.stem_w = None
-        if (stem == "fused" and self.fuse_stem and self.pool == (3, 2, 1) and
+        self.stem_exact = None
+        if (stem in ("fused", "split") and self.fuse_stem and self.pool == (3, 2, 1) and
                 isinstance(c1, nn.Conv2d)
                 and type(c1) is nn.Conv2d and c1.in_channels == 3 and c1.out_channels == 64
                 and c1.kernel_size == (7, 7) and c1.stride == (2, 2) and c1.padding == (3, 3)
@@ -219,6 +223,8 @@ class FusedResNet(nn.Module):
                 self.stem_w = tq_ops.pack_stem_weight(c1.weight)
             except RuntimeError:  # weights outside the fp16 split's range: unfused stem
                 self.stem_w = None
+            if self.stem_w is not None and stem == "fused":
+                self.stem_exact = tq_ops.pack_stem_exact(c1.weight)
 
     def _stem_fused(self, x, first):
         n, _, h, w = x.shape
@@ -231,13 +237,17 @@ class FusedResNet(nn.Module):
         if first.down is not None and not shared:
             codes_down = torch.empty((n, h // 4, w // 4, first.down.cp_in),
                                      dtype=first.down.code_dtype, device=x.device)
+        ws = None
+        if self.stem_exact is not None:
+            ws = tq_native.stem_workspace(n, h, w, x.device)
         # work = the stem conv's fp32 MACs (7x7x3 per output of the 64 x H/2 x W/2 conv)
         tq_ops._launch(
             "stem_conv_pool", n * 64 * (h // 2) * (w // 2) * 147,
             lambda: tq_native.stem_conv_pool_encode(
                 x, self.stem_w, self.stem_scale, self.stem_shift, out, codes_a=codes,
                 quant_a=first.conv1.quant, codes_b=codes_down,
-                quant_b=first.down.quant if codes_down is not None else None))
+                quant_b=first.down.quant if codes_down is not None else None,
+                exact=self.stem_exact, workspace=ws))
         return out, codes, (codes if shared else codes_down)
 
     def _stem(self, x):

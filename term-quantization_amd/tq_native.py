@@ -99,7 +99,8 @@ _SIGNATURES["tq_dwconv2d_termpair_fused"] = [
 
 _SIGNATURES["tq_stem_conv_pool_encode"] = [
     _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _i32,
-    _vp, _i64, _f32, _i32, _i32, _i32, _vp]
+    _vp, _i64, _f32, _i32, _i32, _i32, _vp, _vp, _vp, _i64, _vp]
+_SIGNATURES["tq_stem_workspace_bytes"] = [_i64, _i64, _i64]
 _SIGNATURES["tq_conv2d_termpair_f16"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
     _i64, _f64, _vp, _vp, _i64, _i64, _i32, _i32, _i32, ctypes.POINTER(ConvEpilogue), _vp]
@@ -555,15 +556,30 @@ def conv2d_workspace(pixels, cout, device):
     return torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=device)
 
 
+def stem_workspace(n, h, w, device):
+    """Scratch of the fused stem's exact fix-up (uint8 tensor, tq_stem_workspace_bytes)."""
+    nbytes = int(lib().tq_stem_workspace_bytes(int(n), int(h), int(w)))
+    if nbytes < 0:
+        raise ValueError("stem_workspace: invalid image size %dx%dx%d" % (n, h, w))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
 def stem_conv_pool_encode(x, w_split, scale, shift, out, codes_a=None, quant_a=None,
-                          codes_b=None, quant_b=None):
+                          codes_b=None, quant_b=None, exact=None, workspace=None):
     """relu(maxpool(bn(conv7x7s2(x)))) of a ResNet stem into ``out`` plus next layers' codes
     (tq_stem_conv_pool_encode); x fp32 channels_last [N, 3, H, W], w_split from
-    tq_ops.pack_stem_weight."""
+    tq_ops.pack_stem_weight.  ``exact`` = (w64, wbound) from tq_ops.pack_stem_exact turns on
+    the exact fix-up of near-midpoint outputs (workspace: stem_workspace, allocated here when
+    None); without it the split-fp16 conv's result stands."""
     n, c, h, w = x.shape
     ho, wo = out.shape[2], out.shape[3]
     qa = quant_a or (0.0, 0, 0)
     qb = quant_b or (0.0, 0, 0)
+    w64 = wbound = None
+    if exact is not None:
+        w64, wbound = exact
+        if workspace is None:
+            workspace = stem_workspace(n, h, w, x.device)
     with torch.cuda.device(x.device):
         rc = lib().tq_stem_conv_pool_encode(
             _ptr(x), n, h, w, _ptr(w_split), _ptr(scale), _ptr(shift), _ptr(out), ho, wo,
@@ -571,7 +587,8 @@ def stem_conv_pool_encode(x, w_split, scale, shift, out, codes_a=None, quant_a=N
             int(qa[1]), int(qa[2]), code_format(codes_a) if codes_a is not None else 0,
             _ptr(codes_b), codes_b.shape[-1] if codes_b is not None else 0, float(qb[0]),
             int(qb[1]), int(qb[2]), code_format(codes_b) if codes_b is not None else 0,
-            _stream(x))
+            _ptr(w64), _ptr(wbound), _ptr(workspace if exact is not None else None),
+            workspace.numel() if (exact is not None) else 0, _stream(x))
     _check(rc)
     return out
 

@@ -88,3 +88,18 @@ def test_spawn_stops_the_other_ranks_when_one_fails(tmp_path):
         assert time.monotonic() - t0 < 60
     finally:
         bench.os.path.abspath = orig
+
+
+def test_check_world_counts_this_nodes_ranks(monkeypatch):
+    """check_world compares the ranks of this node (LOCAL_WORLD_SIZE) with its GPUs, so a
+    multi-node torchrun (WORLD_SIZE 16 over 2 x 8 GPUs) passes on every rank, while more local
+    ranks than GPUs, or a local rank past the last GPU, fail."""
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert bench.check_world(16, 7)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "9")
+    assert not bench.check_world(16, 0)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert bench.check_world(8, 3)
+    assert not bench.check_world(9, 3)
+    assert not bench.check_world(4, 8)

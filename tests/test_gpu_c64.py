@@ -102,8 +102,9 @@ def test_c64_bit_identical_to_valu(hw, batch, grid, monkeypatch):
 
 def test_c64_partial_last_tile(monkeypatch):
     """N*H*W = 3 * 56^2 = 9408 = 36.75 tiles: the last tile's upper 64 pixels (two waves'
-    blocks) are past the tensor -- their taps read the zero pixel, their stores are dropped;
-    the guard rows of the output buffers stay untouched."""
+    blocks) lie past the tensor; the waves that would own them return before their epilogue
+    (tr_conv_c64.hip), so the outputs are the VALU engine's bits (the guard tail behind every
+    buffer: test_c64_partial_last_tile_leaves_guard_untouched)."""
     conv, x, sc, sh, res = _case(56, 3, seed=5)
     lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
     ref = _run(cv, lay_v, 56, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16)
@@ -156,14 +157,19 @@ def test_c64_bench_size_default_grid(batch, monkeypatch):
 @pytest.mark.parametrize("seed", range(8))
 def test_c64_random_sweep(seed, monkeypatch):
     """Seeded random layer-1 engine cases (maps 3-63 -- the widest halo the engine takes --,
-    batch 1-12, persistent grids of 1 / 2 / 3 / 37 / default workgroups, every epilogue form):
-    bit-identical to the VALU engine."""
+    persistent grids of 1 / 2 / 3 / 37 / default workgroups, every epilogue form), the batch
+    drawn so that N*H*W is a multiple of the engine's 32-pixel block (the shapes it takes):
+    bit-identical to the VALU engine.  TQ_CONFIG_STRICT=1 makes config 15 fail instead of
+    falling back to the default engine, so every case runs the c64 engine itself."""
+    import math
     import numpy as np
     rng = np.random.default_rng(8000 + seed)
     hw = int(rng.integers(3, 64))
-    batch = int(rng.integers(1, 13))
+    unit = 32 // math.gcd(hw * hw, 32)
+    batch = unit * int(rng.integers(1, max(2, 12 // unit + 1)))
     conv, x, sc, sh, res = _case(hw, batch, seed=8000 + seed)
     lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    monkeypatch.setenv("TQ_CONFIG_STRICT", "1")
     monkeypatch.setenv("TQ_C64_GRID", str(int(rng.choice([0, 1, 2, 3, 37]))))
     form = sorted(FORMS)[int(rng.integers(0, len(FORMS)))]
     kw = dict(FORMS[form])
@@ -173,3 +179,68 @@ def test_c64_random_sweep(seed, monkeypatch):
     got = _run(cm, lay_m, hw, cfg=C64, sc=sc, sh=sh, kc_steps=lay_m.kc_steps, **kw)
     for g, r in zip(got, ref):
         assert (g is None and r is None) or torch.equal(g, r), form
+
+
+def test_c64_strict_mode_rejects_an_ineligible_shape(monkeypatch):
+    """The dispatch probe behind the random sweep: with TQ_CONFIG_STRICT=1 config 15 on a
+    shape the engine cannot take (N*H*W = 9 * 9 = 81, not a multiple of 32) is an error, and
+    without it the conv quietly runs the default engine."""
+    conv, x, sc, sh, res = _case(9, 1, seed=3)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, 9, cfg=0, sc=sc, sh=sh, fmt=torch.int16)
+    got = _run(cm, lay_m, 9, cfg=C64, sc=sc, sh=sh, kc_steps=lay_m.kc_steps)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    monkeypatch.setenv("TQ_CONFIG_STRICT", "1")
+    with pytest.raises(RuntimeError):
+        _run(cm, lay_m, 9, cfg=C64, sc=sc, sh=sh, kc_steps=lay_m.kc_steps)
+
+
+def test_c64_partial_last_tile_leaves_guard_untouched(monkeypatch):
+    """Output buffers with a 64 KB guard tail behind the tensor (fp32 output, both code
+    outputs) on the partial-last-tile shape: every grid writes exactly the tensor."""
+    conv, x, sc, sh, res = _case(56, 3, seed=5)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    ref = _run(cv, lay_v, 56, cfg=0, sc=sc, sh=sh, res=res, fmt=torch.int16, codes_b=True)
+    n, hw, g = 3, 56, 16384
+    monkeypatch.setenv("TQ_CONFIG_STRICT", "1")
+    for grid in ("0", "2", "37"):
+        monkeypatch.setenv("TQ_C64_GRID", grid)
+        ob = torch.full((n * hw * hw * 64 + g,), float("nan"), device=DEV)
+        o = ob[:n * hw * hw * 64].view(n, hw, hw, 64).permute(0, 3, 1, 2)
+        cab = torch.full((n * hw * hw * 64 + g,), 7, dtype=torch.int16, device=DEV).to(
+            torch.float16)
+        cbb = cab.clone()
+        ca = cab[:n * hw * hw * 64].view(n, hw, hw, 64)
+        cb = cbb[:n * hw * hw * 64].view(n, hw, hw, 64)
+        tq_native.conv2d_termpair_fused(cm, lay_m.w_codes, 64, 3, 3, (1, 1), (1, 1), (1, 1),
+                                        hw, hw, out=o, ch_scale=sc, ch_shift=sh, residual=res,
+                                        relu=True, codes_a=ca, quant_a=(0.05, 9, 3),
+                                        codes_b=cb, quant_b=(0.11, 9, 2), config=C64,
+                                        kc_steps=lay_m.kc_steps, kc_chunk=-1)
+        torch.cuda.synchronize()
+        assert torch.equal(o.contiguous(memory_format=torch.channels_last).view(torch.int32)
+                           .cpu(), ref[0]), grid
+        assert torch.equal(ca.float().cpu(), ref[1]) and torch.equal(cb.float().cpu(),
+                                                                      ref[2]), grid
+        assert bool(torch.isnan(ob[n * hw * hw * 64:]).all()), grid
+        assert bool((cab[n * hw * hw * 64:] == 7).all()) and bool(
+            (cbb[n * hw * hw * 64:] == 7).all()), grid
+
+
+@pytest.mark.parametrize("form", ["conv1", "conv2_out", "conv2_codes"])
+def test_epi_fast_off_routes_layer1_forms_bit_identically(form, monkeypatch):
+    """TQ_EPI_FAST=0 (the generic-epilogue A/B switch) turns the c64 default off for the
+    layer-1 forms and the ring engine's forms over to the generic epilogue; the bits stay the
+    VALU engine's."""
+    conv, x, sc, sh, res = _case(28, 4, seed=21)
+    lay_v, cv, lay_m, cm = _layers(conv, x, monkeypatch)
+    kw = dict(FORMS[form])
+    if kw.pop("res", False):
+        kw["res"] = res
+    ref = _run(cv, lay_v, 28, cfg=0, sc=sc, sh=sh, fmt=torch.int16, **kw)
+    monkeypatch.setenv("TQ_EPI_FAST", "0")
+    for ring in ("0", "1"):
+        monkeypatch.setenv("TQ_RING", ring)
+        got = _run(cm, lay_m, 28, cfg=0, sc=sc, sh=sh, kc_steps=lay_m.kc_steps, **kw)
+        for gg, r in zip(got, ref):
+            assert (gg is None and r is None) or torch.equal(gg, r), (form, ring)

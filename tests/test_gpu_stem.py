@@ -127,3 +127,102 @@ def test_stem_row_carry_is_bit_identical_to_separate_tiles():
         torch.cuda.synchronize()
         assert torch.equal(out[i].view(torch.int32), o1[0].view(torch.int32)), i
         assert torch.equal(codes[i].view(torch.int16), c1[0].view(torch.int16)), i
+
+
+def _exact_codes(x, wt, sc, sh, quant):
+    """Codes of the correctly rounded stem: fp64 conv (exact products, fp64 sum) rounded once
+    to fp32, BN as one fp32 fma (emulated in 80-bit long double: the product is exact, then
+    a single rounding to fp32), ReLU, max-pool 3x3/2 pad 1, then oracle.tr.  Returns (fp32
+    pooled values NCHW, integer codes NCHW)."""
+    sf, bw, dt = quant
+    z = F.conv2d(x.double(), wt.double(), None, 2, 3).float().numpy()
+    ld = np.longdouble
+    y = (z.astype(ld) * sc.detach().numpy().astype(ld).reshape(1, -1, 1, 1) +
+         sh.detach().numpy().astype(ld).reshape(1, -1, 1, 1)).astype(np.float32)
+    y = np.maximum(y, np.float32(0.0))
+    pooled = F.max_pool2d(torch.from_numpy(y), 3, 2, 1).numpy()
+    yq = oracle.tr(np.ascontiguousarray(pooled).reshape(1, -1, 1, 1), sf, bw, 1, dt)
+    return pooled, np.rint(yq.reshape(pooled.shape) / np.float32(sf)).astype(np.int64)
+
+
+def _exact_case(n, h, w, fmt, xs, seed, quant, scale_bands=False):
+    sf, bw, dt = quant
+    torch.manual_seed(seed)
+    x = torch.randn(n, 3, h, w) * xs
+    if scale_bands:  # tiles of very different max |x| (the error bound is per tile)
+        x[:, :, h // 5:h // 3] *= 1e-3
+        x[:, :, h // 2:h // 2 + 6] *= 30.0
+    x = x.contiguous(memory_format=torch.channels_last)
+    wt = torch.empty(64, 3, 7, 7)
+    nn.init.kaiming_normal_(wt, mode="fan_out", nonlinearity="relu")
+    sc, sh = _bn_coefs(seed)
+    sc, sh = sc.detach(), sh.detach()
+    ho, wo = h // 4, w // 4
+    out = torch.full((n, 64, ho, wo), float("nan"), device=DEV).contiguous(
+        memory_format=torch.channels_last)
+    codes = torch.zeros((n, ho, wo, 64), dtype=fmt, device=DEV)
+    wsplit = tq_ops.pack_stem_weight(wt.to(DEV))
+    exact = tq_ops.pack_stem_exact(wt.to(DEV))
+    tq_native.stem_conv_pool_encode(x.to(DEV), wsplit, sc.to(DEV), sh.to(DEV), out,
+                                    codes_a=codes, quant_a=quant, exact=exact)
+    codes_split = torch.zeros_like(codes)
+    out_split = torch.empty_like(out)
+    tq_native.stem_conv_pool_encode(x.to(DEV), wsplit, sc.to(DEV), sh.to(DEV), out_split,
+                                    codes_a=codes_split, quant_a=quant)
+    pooled, exp = _exact_codes(x, wt, sc, sh, quant)
+    got = codes.cpu().long().permute(0, 3, 1, 2).numpy()
+    split = codes_split.cpu().long().permute(0, 3, 1, 2).numpy()
+    # every code is the correctly rounded conv's code
+    assert np.array_equal(got, exp), int((got != exp).sum())
+    # and still TR of the fp32 output the kernels wrote (the fix-up rewrites both)
+    yq = oracle.tr(out.contiguous().cpu().numpy().reshape(1, -1, 1, 1), sf, bw, 1, dt)
+    assert np.array_equal(np.rint(yq.reshape(out.shape) / np.float32(sf)).astype(np.int64), got)
+    # outputs the fix-up did not touch are the split kernel's bits; the others the exact value
+    o = out.cpu().numpy()
+    os_ = out_split.cpu().numpy()
+    touched = o.view(np.int32) != os_.view(np.int32)
+    assert np.array_equal(o[touched], pooled[touched])
+    return int((split != exp).sum()), int(touched.sum()), got.size
+
+
+@pytest.mark.parametrize("n,h,w,fmt,xs,bands", [(2, 224, 224, torch.float16, 1.0, False),
+                                                (3, 32, 48, torch.int16, 2.0, False),
+                                                (2, 20, 296, torch.float16, 3e3, False),
+                                                (4, 224, 224, torch.float16, 1.0, True),
+                                                (1, 64, 36, torch.float16, 1e-3, True)])
+def test_stem_exact_fixup_gives_the_correctly_rounded_codes(n, h, w, fmt, xs, bands):
+    """The exact fix-up (tq_ops.pack_stem_exact): every code equals the code of the correctly
+    rounded fp32 conv -> the same BN fma -> ReLU -> max-pool, on shapes where the split-fp16
+    result alone flips codes.  sf is small (0.002: 9-bit codes span ~1, so many quotients sit
+    near midpoints) to exercise the fix-up heavily."""
+    flips_split, touched, total = _exact_case(n, h, w, fmt, xs, 900 + h + w, (0.002, 9, 3),
+                                              bands)
+    print("exact stem %dx%dx%d: split-only flips %d, fixed-up outputs %d of %d"
+          % (n, h, w, flips_split, touched, total))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_stem_exact_fixup_random_sweep(seed):
+    """Seeded random shapes, input scales and TR settings for the exact fix-up."""
+    rng = np.random.default_rng(7000 + seed)
+    h = 4 * int(rng.integers(2, 59))
+    w = 4 * int(rng.integers(2, 113))
+    fmt = torch.float16 if rng.random() < 0.7 else torch.int16
+    xs = float(10.0 ** rng.uniform(-3, 3))
+    quant = (float(10.0 ** rng.uniform(-3, -1)) * xs, int(rng.integers(6, 12)),
+             int(rng.integers(1, 5)))
+    _exact_case(int(rng.integers(1, 4)), h, w, fmt, xs, 7000 + seed, quant,
+                bool(rng.random() < 0.5))
+
+
+def test_stem_exact_rejects_partial_args():
+    x = torch.zeros((1, 3, 32, 32), device=DEV).contiguous(memory_format=torch.channels_last)
+    out = torch.zeros((1, 64, 8, 8), device=DEV).contiguous(memory_format=torch.channels_last)
+    wt = torch.zeros(64, 3, 7, 7, device=DEV)
+    wsplit = tq_ops.pack_stem_weight(wt)
+    w64, wb = tq_ops.pack_stem_exact(wt)
+    sc = torch.ones(64, device=DEV)
+    small = torch.empty(16, dtype=torch.uint8, device=DEV)
+    with pytest.raises(RuntimeError, match="workspace too small"):
+        tq_native.stem_conv_pool_encode(x, wsplit, sc, sc, out, exact=(w64, wb),
+                                        workspace=small)

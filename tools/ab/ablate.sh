@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build timing-only ablation variants of libtq_hip.so (never loaded by the product: select
-# one with TQ_LIB_PATH).  Usage: bash tools/ablate.sh 1 2  -> lib/libtq_hip_abl1.so, ...
+# one with TQ_LIB_PATH).  Usage: bash tools/ab/ablate.sh 1 2  -> lib/libtq_hip_abl1.so, ...
 set -e
 cd "$(dirname "$0")/../term-quantization_amd"
 for V in "$@"; do

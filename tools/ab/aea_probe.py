@@ -1,6 +1,6 @@
 """Time tq_act_encode_act (gate, no act: EfficientNet-b0's project-conv input pass) on the
 dw output shapes of EfficientNet-b0 at a 128-image chunk; select a build with TQ_LIB_PATH.
-    python tools/aea_probe.py [--iters 20]"""
+    python tools/ab/aea_probe.py [--iters 20]"""
 import argparse
 import os
 import sys

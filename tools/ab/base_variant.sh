@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build lib/libtq_hip_<name>.so from the csrc/ of a git revision (default HEAD), for A/B
 # timing of working-tree kernel changes against it (select with TQ_LIB_PATH; never loaded by
-# the product).  Usage: bash tools/base_variant.sh [rev] [name]
+# the product).  Usage: bash tools/ab/base_variant.sh [rev] [name]
 set -e
 REV=${1:-HEAD}; NAME=${2:-base}
 cd "$(dirname "$0")/../term-quantization_amd"

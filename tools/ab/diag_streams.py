@@ -5,7 +5,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "term-quantization_amd"))
 os.environ["TQ_CONV_ENGINE"] = "mfma"
@@ -18,7 +18,7 @@ dev = torch.device("cuda:0")
 _, qmodel, _ = bench.build_model(dev, 256, 0)
 x, _ = util.SyntheticImageNet(512, 256, seed=0, device=dev).batch(0)
 x = x.contiguous(memory_format=torch.channels_last)
-fused = tq_fuse.FusedResNet(qmodel)
+fused = tq_fuse.FusedResNet(qmodel, stem="split")  # (the r05 stem: no fix-up)
 for flag in ("1", "0"):
     os.environ["TQ_C64"] = flag
     with torch.no_grad():

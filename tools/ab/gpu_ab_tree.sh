@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved bench A/B of this tree against another checkout of the repo (a git worktree
 # under _ab/<name>, built in place): same lease, same box, alternating runs.
-# Usage: bash tools/gpu_ab_tree.sh <tag> <rounds> <worktree dir> [bench args...]
+# Usage: bash tools/ab/gpu_ab_tree.sh <tag> <rounds> <worktree dir> [bench args...]
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; TAG=$1; N=$2; ALT=$3; shift 3; O=$R/gpurun_out/$TAG
 mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of c64 engine variant builds (tools/variant1.sh) on the layer-1 conv forms, interleaved,
-# two rounds.  Usage: bash tools/gpu_c64_ab.sh <tag> <variant>...
+# A/B of c64 engine variant builds (tools/ab/variant1.sh) on the layer-1 conv forms, interleaved,
+# two rounds.  Usage: bash tools/ab/gpu_c64_ab.sh <tag> <variant>...
 set -u
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=gpurun_out/$TAG; mkdir -p $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the ring engine's DMA placement (RING_DMA_LATE variant build vs the product build):
 # ring parity tests on the variant, then interleaved tools/layer_times.py runs.
-# Usage: bash tools/gpu_dmalate_ab.sh <tag>   (variant: bash tools/variant.sh dmalate ...)
+# Usage: bash tools/ab/gpu_dmalate_ab.sh <tag>   (variant: bash tools/ab/variant.sh dmalate ...)
 set -u
 TAG=${1:-dmalate}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=gpurun_out/$TAG; mkdir -p $O

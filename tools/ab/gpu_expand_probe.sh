@@ -1,7 +1,7 @@
 #!/bin/bash
 # MobileNet-V2 / EfficientNet-b0 expand-conv shapes (1x1, small Cin -> large Cout, codes-only
 # epilogue): config 0 (the heuristic, which picks the expand engine for these shapes) and 10
-# (the direct engine), optionally against a variant build.  Usage: bash tools/gpu_expand_probe.sh [variant]
+# (the direct engine), optionally against a variant build.  Usage: bash tools/ab/gpu_expand_probe.sh [variant]
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; V=${1:-}
 for S in 16,96,1,1,112 24,144,1,1,56 32,192,1,1,28 40,240,1,1,28 64,384,1,1,14 80,480,1,1,14 96,576,1,1,14 112,672,1,1,14 160,960,1,1,7; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Layer-1 conv baseline at HEAD: per-launch times of the fused executor, the layer-1 conv
 # forms on their default engines (conv_probe), and one SQ counter pass per form.
-# Usage: bash tools/gpu_l1_base.sh <tag>
+# Usage: bash tools/ab/gpu_l1_base.sh <tag>
 set -u
 TAG=${1:-l1base}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=gpurun_out/$TAG; mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Layer-1 (64 -> 64, 56x56) 3x3 conv: default engines vs the tap-ring engine (config 13) for
-# the codes-only and residual epilogue forms.  Usage: bash tools/gpu_l1_ring.sh
+# the codes-only and residual epilogue forms.  Usage: bash tools/ab/gpu_l1_ring.sh
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"
 for F in "--no-out" "--residual"; do

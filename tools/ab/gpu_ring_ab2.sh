@@ -1,6 +1,6 @@
 #!/bin/bash
 # Ring-engine timing ablations (libtq_hip_<variant>.so) for both epilogue forms.
-# Usage: bash tools/gpu_ring_ab2.sh "<layers>" "<variants>"
+# Usage: bash tools/ab/gpu_ring_ab2.sh "<layers>" "<variants>"
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; LAYERS=$1; VARS=$2
 for L in $LAYERS; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Ring shapes side by side: per-layer timings of the default engines, shape 1 and shape 2 for
-# both epilogue forms.  Usage: bash tools/gpu_ring_cmp.sh <tag> "<layers>"
+# both epilogue forms.  Usage: bash tools/ab/gpu_ring_cmp.sh <tag> "<layers>"
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; TAG=${1:-cmp}; LAYERS=${2:-"6 8 11 13 16 18"}
 for L in $LAYERS; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a timing variant of libtq_hip.so with extra compile flags (never loaded by the
-# product: select it with TQ_LIB_PATH).  Usage: bash tools/variant.sh NAME "-DFOO=1 ..."
+# product: select it with TQ_LIB_PATH).  Usage: bash tools/ab/variant.sh NAME "-DFOO=1 ..."
 #   -> term-quantization_amd/lib/libtq_hip_NAME.so
 set -e
 cd "$(dirname "$0")/../term-quantization_amd"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a timing variant of libtq_hip.so that recompiles ONE kernel source with extra flags and
 # links it with the product objects of the others (never loaded by the product: select it with
-# TQ_LIB_PATH).  Usage: bash tools/variant1.sh NAME SOURCE "-DFOO=1 ..."
+# TQ_LIB_PATH).  Usage: bash tools/ab/variant1.sh NAME SOURCE "-DFOO=1 ..."
 #   -> term-quantization_amd/lib/libtq_hip_NAME.so
 set -e
 cd "$(dirname "$0")/../term-quantization_amd"

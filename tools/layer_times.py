@@ -4,7 +4,7 @@
 
 HIP events around every TQ kernel on its launch stream; prints the average duration of each
 launch position over the steps, with its layer shape.  With TQ_LIB_PATH pointing at an
-ablation build (tools/ablate.sh) it shows what each part of a kernel costs (timing only)."""
+ablation build (tools/ab/ablate.sh) it shows what each part of a kernel costs (timing only)."""
 import argparse
 import os
 import sys

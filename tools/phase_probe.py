@@ -1,5 +1,5 @@
 """Per-workgroup phase timing of one term-pair conv launch (direct engine), from the timing-only
-build `bash tools/variant.sh trace -DTQ_PHASE_TRACE=1` (s_memrealtime stamps at workgroup start,
+build `bash tools/ab/variant.sh trace -DTQ_PHASE_TRACE=1` (s_memrealtime stamps at workgroup start,
 main-loop end and epilogue end; select the build with TQ_LIB_PATH).
 
     TQ_LIB_PATH=$PWD/term-quantization_amd/lib/libtq_hip_trace.so \\

@@ -1,5 +1,5 @@
 """Per-tile phase timing of one tap-ring conv launch, from the timing-only build
-`bash tools/variant1.sh rtrace tr_conv_ring "-DRING_TRACE=1"` (wave 0's s_memrealtime stamps per
+`bash tools/ab/variant1.sh rtrace tr_conv_ring "-DRING_TRACE=1"` (wave 0's s_memrealtime stamps per
 tile: start, first barrier passed, K loop done, epilogue issued; select it with TQ_LIB_PATH).
 
     TQ_LIB_PATH=$PWD/term-quantization_amd/lib/libtq_hip_rtrace.so \\

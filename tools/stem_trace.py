@@ -1,5 +1,5 @@
 """Per-tile phase timing of one fused-stem launch at the bench batch, from the timing-only build
-`bash tools/variant1.sh strace tq_stem_conv "-DSTEM_TRACE=1"` (wave 0's s_memrealtime stamps per
+`bash tools/ab/variant1.sh strace tq_stem_conv "-DSTEM_TRACE=1"` (wave 0's s_memrealtime stamps per
 tile: loop top, barrier A passed (tile max known), barrier B passed (rows committed), tile done;
 select it with TQ_LIB_PATH).   python tools/stem_trace.py"""
 import ctypes
