@@ -40,10 +40,10 @@ import util  # noqa: E402
 
 METRIC = "term-pair MACs/sec + images/sec, ResNet-18 TQ g=8 at 1/2/4/8 MI355X"
 WB, G, K, DB, DT = 9, 8, 12, 9, 3
-STEM_NAMES = {"fused": "fp32-exact codes (fused stem kernel: split-fp16 MFMA conv + exact fp64 "
-                       "recompute of every output within the split's error bound of a "
-                       "rounding midpoint)",
-              "split": "split-fp16 near-fp32 (fused stem kernel, no fix-up)",
+STEM_NAMES = {"fused": "split-fp16 near-fp32 (fused stem kernel; its codes sit closer to the "
+                       "correctly rounded conv's than torch's fp32 convs do, DESIGN 3)",
+              "exact": "correctly rounded codes (fused stem kernel + exact fp64 recompute of "
+                       "every output within the split's error bound of a rounding midpoint)",
               "fp32": "torch fp32 conv (MIOpen) + BN/ReLU/max-pool/codes kernel"}
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 HBM_BYTES_PER_IMAGE = 15026432   # algorithmic bytes of the TR path per image
@@ -84,11 +84,11 @@ def parse(argv=None):
     ap.add_argument("--no-d4", action="store_true",
                     help="skip the d4 key (BASELINE configs[2]/[3]: LSTM-650, fused "
                          "MobileNet-V2 / EfficientNet-b0; rank 0 at N=1 only)")
-    ap.add_argument("--stem", choices=("fused", "split", "fp32"), default="fused",
-                    help="fused: the fused stem kernel + its exact fix-up (codes of the "
-                         "correctly rounded fp32 conv); split: the fused stem kernel alone "
-                         "(split-fp16 near-fp32); fp32: torch's fp32 conv + the "
-                         "BN/ReLU/max-pool/codes kernel")
+    ap.add_argument("--stem", choices=("fused", "exact", "fp32"), default="fused",
+                    help="fused: the fused stem kernel (split-fp16 near-fp32); exact: the "
+                         "fused stem kernel + its exact fix-up (codes of the correctly rounded "
+                         "fp32 conv); fp32: torch's fp32 conv + the BN/ReLU/max-pool/codes "
+                         "kernel")
     ap.add_argument("--no-stem-leg", action="store_true",
                     help="skip the second timed pass with the other stem (N=1 only)")
     ap.add_argument("--unfused", action="store_true",
@@ -550,16 +550,19 @@ def main(argv=None):
         # GPU time of that one-stream pass (its kernels plus the event gaps between them)
         roof_pass_s = timer.base.elapsed_time(pass_end) * 1e-3
 
-        # the other stem: the same executor with the torch fp32 stem conv
-        # (MIOpen, true fp32) + the BN/ReLU/max-pool/codes kernel, timed the same way -- the
-        # price of the fused split-fp16 stem's precision choice, reported beside the headline
-        stem_leg = None
+        # the other stems: the same executor with the torch
+        # fp32 stem conv (MIOpen, true fp32) + the BN/ReLU/max-pool/codes kernel, and with the
+        # fused stem's exact fix-up, timed the same way, reported beside the headline
+        stem_legs = {}
         if world == 1 and not args.unfused and not args.no_stem_leg:
-            other = "fused" if args.stem == "fp32" else "fp32"
-            el2, launch2, _ = timed_steps(tq_fuse.FusedResNet(qmodel, stem=other))
-            stem_leg = {"stem": STEM_NAMES[other], "images_per_s": args.batch * args.steps / el2,
-                        "ms_per_step": el2 / args.steps * 1e3, "launch": launch2,
-                        "streams": args.streams}
+            for other in ("fp32", "exact", "fused"):
+                if other == args.stem:
+                    continue
+                el2, launch2, _ = timed_steps(tq_fuse.FusedResNet(qmodel, stem=other))
+                stem_legs["stem_" + other] = {
+                    "stem": STEM_NAMES[other], "images_per_s": args.batch * args.steps / el2,
+                    "ms_per_step": el2 / args.steps * 1e3, "launch": launch2,
+                    "streams": args.streams}
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -656,7 +659,7 @@ def main(argv=None):
                           "activation TR -> fp16 codes)" + (
                               " + stem_fixup_kernel (exact fp64 recompute of the listed "
                               "near-midpoint outputs; time included)"
-                              if args.stem == "fused" else ""),
+                              if args.stem == "exact" else ""),
                 "bound": "mfma",
                 # what the matrix cores execute: 3 fp16 split products per fp32 MAC, against
                 # the dense fp16 MFMA peak
@@ -723,8 +726,7 @@ def main(argv=None):
             "roofline_tr": roof_tr,
             "accuracy_counters": acc_counters,
         }
-        if stem_leg is not None:
-            result["stem_fused" if args.stem == "fp32" else "stem_fp32"] = stem_leg
+        result.update(stem_legs)
         if world == 1 and not args.no_d1:
             result["d1_tr_op"] = d1_tr_op(dev)
         if world == 1 and not args.no_d4:

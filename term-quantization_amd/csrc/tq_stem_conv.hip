@@ -60,6 +60,15 @@
 #ifndef STEM_PF
 #define STEM_PF 0  // 1: the next K-step's input slices read during this step's MFMAs
 #endif
+#ifndef STEM_NRM_MFMA
+#define STEM_NRM_MFMA 1  // window norms: 1 the diagonal of an MFMA, 0 v_dot2 on the VALU
+#endif
+#ifndef FIXUP_AB
+#define FIXUP_AB 0  // timing-only builds of the fix-up kernel: 1 no sums, 2 no window staging
+#endif
+#ifndef STEM_FIXAB
+#define STEM_FIXAB 0  // timing-only builds of the fix-up listing: 1 no window norms, 2 no flags
+#endif
 
 namespace tq {
 
@@ -95,13 +104,27 @@ __device__ __forceinline__ float row_down(float v) {
 
 // ONE: one strip per wave (nb <= 8 waves: Wo <= 56), the strip's last conv row carried to
 // the next tile (STEM_CARRY)
-template <int TP, int QMAX, bool ONE>
+// sum of squares of an 8-value fp16 slice, added to acc (v_dot2_f32_f16)
+__device__ __forceinline__ float sq8(const f16x8& v, float acc) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const h2 p = {v[2 * i], v[2 * i + 1]};
+    acc = __builtin_amdgcn_fdot2(p, p, acc, false);
+  }
+  return acc;
+}
+
+// FIX: the exact fix-up's listing (a.fix_list): each conv output's input-window norm is summed
+// beside its MFMAs, pooled like the values, and bounds the split conv's error.
+template <int TP, int QMAX, bool ONE, bool FIX>
 __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArgs a, int sc,
                                                                          int nb, int tiles) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds_raw[];
   __shared__ uint32_t tile_max[2];  // max |x| (fp32 bits) of a tile's rows, by tile parity
   __shared__ uint32_t fix_n;        // near-midpoint outputs this workgroup listed (fix-up)
-  __shared__ float fix_ew[2][64];   // per side and channel: quotient error per unit max |x|
+  __shared__ float fix_ew[2][64];   // per side and channel: quotient error per unit norm
+  __shared__ float fix_nrm[8][8];   // per wave: pooled window norms^2 of the strip's 7 pixels
   uint16_t* ws = reinterpret_cast<uint16_t*>(lds_raw);
   float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(lds_raw) + kStemWBytes);
   // per-wave pool staging: 7 pixels x 64 channels fp32 behind the input rows
@@ -142,15 +165,17 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
     bsc[i] = fabsf(a.scale[4 * i16 + i]);
     bsh[i] = a.shift[4 * i16 + i];
   }
-  // Exact fix-up (a.fix_list): the split conv of channel c is within wbound[c] * M of the
-  // exact sum, M the max |x| of the input rows it read, so an output whose quotient y / sf
-  // lies within M * ew[c] (+ two ulps of slack for the BN fma and the quotient's rounding) of
-  // a rounding midpoint is the only kind whose code can differ from the exact conv's; those
-  // are listed for stem_fixup_kernel, which recomputes them exactly.
-  const bool fix = a.fix_list != nullptr;
+  // Exact fix-up (FIX): the split conv of channel c at a conv position is within wbound[c] *
+  // |x| of the exact sum (|x| the 2-norm of the position's input window; wbound[c] = the
+  // relative error bound times |w[c]|_2, Cauchy-Schwarz), so a pooled output whose quotient
+  // y / sf lies within that (through BN, with the window norms pooled like the values, +
+  // two ulps of slack for the BN fma and the quotient's rounding) of a rounding midpoint is
+  // the only kind whose code can differ from the exact conv's; those are listed for
+  // stem_fixup_kernel, which recomputes them exactly.
+  constexpr bool fix = FIX;
   if (fix && tid < 128) {  // visible after the first barrier
     const int c = tid & 63;
-    const float wb = a.wbound[c] * fabsf(a.scale[c]) * 1.0009765625f;
+    const float wb = a.wbound[c] * fabsf(a.scale[c]) * 1.00390625f;
     fix_ew[tid >> 6][c] = wb * (float)(tid < 64 ? a.inv_a : a.inv_b);
   }
 
@@ -240,8 +265,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   // one strip per wave (Wo <= 56): each wave keeps its strip's last conv row for the next tile
   constexpr bool one = ONE;
   f32x4 carry[4];
+  float carry_n = 0.0f;  // (FIX) the carried row's window norm^2
   int prev_tile = -2, prev_kx = 0;
-  float prev_tm = 0.0f;
   for (int tile = t_begin; tile < t_end; ++tile, ++it) {
 #if STEM_TRACE
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
@@ -275,11 +300,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       kx = kStemXMag - e;
     }
     const int kback = -(kx + kStemWExp);
-    // the max |x| behind this tile's conv rows (a carried row was read in the previous tile)
-    const float cur_tm = __uint_as_float(mbits);
-    const bool carried = ONE && STEM_CARRY && py0 != 0 && tile == prev_tile + 1 &&
-                         n == prev_tile / tpi && kx == prev_kx;
-    const float tm = carried ? fmaxf(cur_tm, prev_tm) : cur_tm;
+    const float unscale = ldexpf(1.0f, -kx);  // (FIX) window norms back to input units
     if (STEM_AB != 3) commit(kx);  // (3: timing only, no input staging)
     if (tid == 0) tile_max[(it + 1) & 1] = 0u;
     __syncthreads();  // B
@@ -315,13 +336,21 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         h0 = __builtin_shufflevector(a0, b0, 0, 1, 2, 3, 4, 5, 6, 7);
         h1 = __builtin_shufflevector(a1, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       };
-      auto conv_rows = [&](auto nr_tag, int rr, f32x4 (&y)[4][4]) {
+      // (FIX) nrm[r]: sum of x0^2 over the input window of conv row r at column ox (scaled
+      // units; 0 outside the image): the diagonal of one more MFMA per row and K-step, the
+      // slice against itself (D[i][j] = sum_k x_i[k] x_j[k] over the 16 columns i, j)
+      auto conv_rows = [&](auto nr_tag, int rr, f32x4 (&y)[4][4], float (&nrm)[4]) {
         constexpr int NR = decltype(nr_tag)::value;
         f32x4 acc[NR][4];
+        f32x4 sq[FIX && STEM_NRM_MFMA ? NR : 1];
+        float sqv[FIX && !STEM_NRM_MFMA ? NR : 1];
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
+        for (int r = 0; r < NR; ++r) {
+          if constexpr (FIX && STEM_NRM_MFMA) sq[r] = (f32x4)0.0f;
+          if constexpr (FIX && !STEM_NRM_MFMA) sqv[r] = 0.0f;
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) acc[r][mb] = (f32x4)0.0f;
+        }
         auto mfmas = [&](int ks, const f16x8 (&x0)[NR], const f16x8 (&x1)[NR])
             __attribute__((always_inline)) {
 #pragma unroll
@@ -369,6 +398,15 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #pragma unroll
           for (int r = 0; r < NR; ++r) load_x(rr + r, ks, x0[r], x1[r]);
           mfmas(ks, x0, x1);
+          if constexpr (FIX && STEM_FIXAB != 1) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              if constexpr (STEM_NRM_MFMA)
+                sq[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x0[r], x0[r], sq[r], 0, 0, 0);
+              else
+                sqv[r] = sq8(x0[r], sqv[r]);
+            }
+          }
         }
 #endif
         // raw (sign-adjusted) sums; conv positions outside the image pool as -inf
@@ -380,12 +418,27 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
             for (int i = 0; i < 4; ++i) y[r][mb][i] = ok ? acc[r][mb][i] : -__builtin_inff();
+          if constexpr (FIX) {
+            float t;
+            if constexpr (STEM_NRM_MFMA) {
+              // D[i16][i16] sits in lane (i16, i16 / 4), element i16 % 4
+              const int e = i16 & 3;
+              const float d =
+                  e == 0 ? sq[r][0] : e == 1 ? sq[r][1] : e == 2 ? sq[r][2] : sq[r][3];
+              t = __shfl(d, i16 + 16 * (i16 >> 2));
+            } else {
+              t = sqv[r] + __shfl_xor(sqv[r], 16);
+              t += __shfl_xor(t, 32);
+            }
+            nrm[r] = ok ? t : 0.0f;
+          }
         }
       };
 
       // Pool row j = max over conv rows rr = 2j, 2j+1, 2j+2: rows are computed in pairs
       // (2i, 2i+1); row 2i closes pool row i-1 and, with row 2i+1, opens pool row i.
-      auto emit_pool = [&](int j, const f32x4 (&run)[4], const f32x4 (&last)[4]) {
+      auto emit_pool = [&](int j, const f32x4 (&run)[4], const f32x4 (&last)[4], float run_n,
+                           float last_n) {
         const int py = py0 + j;
         if (STEM_AB == 1) {  // timing only: no pool / BN / stores (every conv sum kept live)
           float keep = 0.0f;
@@ -409,6 +462,11 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         // compact the strip's 7 pool pixels x 64 channels through LDS, then every lane
         // finishes 4 consecutive channels of up to two of the 112 quads: contiguous stores
         // and no TR work on the 9 lanes of each row that hold no pool output
+        float mn = 0.0f;  // (FIX) the pool window's largest input-window norm^2
+        if constexpr (FIX) {
+          const float v = fmaxf(run_n, last_n);
+          mn = fmaxf(fmaxf(v, row_down<1>(v)), row_down<2>(v));
+        }
         if (py >= a.Ho) return;
         const int q = i16 >> 1;
         if (!(i16 & 1) && i16 <= 12) {
@@ -416,6 +474,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
           for (int mb = 0; mb < 4; ++mb)
             *reinterpret_cast<f32x4*>(pb + q * 64 + mb * 16 + 4 * g) =
                 (f32x4){m[mb][0], m[mb][1], m[mb][2], m[mb][3]};
+          if (FIX && g == 0) fix_nrm[wave][q] = mn;
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the strip is in LDS
         __builtin_amdgcn_wave_barrier();
@@ -452,13 +511,21 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             const int fmt = side ? a.fmt_b : a.fmt_a;
             uint32_t v[4];
             const uint16_t* lut = side ? lut_b : lut_a;
-            if (fix) {  // near-midpoint quotients, listed for the exact fix-up
+            if constexpr (FIX) {  // near-midpoint quotients, listed for the exact fix-up
               uint32_t fm = 0u;
               const f32x4 ew = *reinterpret_cast<const f32x4*>(&fix_ew[side][co]);
+              // (+ 0.5 scaled units: the fp16 subnormal remainders of inputs below ~2^-17 of
+              // the tile's max, at most 2^-25 each, are not relative to the norm)
+              const float wn = (sqrtf(fix_nrm[wave][f >> 4]) + 0.5f) * unscale;
+              // (an fp32 product is within two ulps of the quotient the codes round: inside
+              // the 2^-12 of slack for quotients below 2^10; past the clamp every code is
+              // maxv's, so a flag there is only a harmless recompute)
+              const float invf = (float)inv;
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
-                const float r = fminf(quotient_f32(yv[i], inv), maxv);
-                if (fabsf(__builtin_amdgcn_fractf(r) - 0.5f) <= fmaf(tm, ew[i], 0x1p-12f))
+                const float r = yv[i] * invf;
+                if (STEM_FIXAB != 2 &&
+                    fabsf(__builtin_amdgcn_fractf(r) - 0.5f) <= fmaf(wn, ew[i], 0x1p-12f))
                   fm |= 1u << i;
               }
               if (fm) ent = ((uint32_t)(p * 16 + (f & 15)) << 4) | (ent & 15u) | fm;
@@ -484,7 +551,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             }
           }
           }
-          if (fix) {  // append the wave's entries to the workgroup's segment
+          if constexpr (FIX) {  // append the wave's entries to the workgroup's segment
             const uint64_t bal = __ballot(ent != 0u);
             if (bal) {
               uint32_t base = 0u;
@@ -507,6 +574,8 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
       // row TP-1.
       f32x4 run[4];
       f32x4 y[4][4];
+      float yn[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // (FIX) the rows' window norms^2
+      float run_n = 0.0f;
       if constexpr (STEM_CARRY && one) {
         // conv row 2 py0 - 1 (rr = 0) is the previous tile's last one (rr = 2 TP) when this
         // wave's previous tile was the one above in the same image (a workgroup walks its
@@ -517,41 +586,45 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
         if (py0 == 0) {
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) carry[mb] = (f32x4)(-__builtin_inff());
+          carry_n = 0.0f;
         } else if (!(tile == prev_tile + 1 && n == prev_tile / tpi && kx == prev_kx)) {
-          conv_rows(std::integral_constant<int, 1>(), 0, y);
+          conv_rows(std::integral_constant<int, 1>(), 0, y, yn);
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) carry[mb] = y[0][mb];
+          carry_n = yn[0];
         }
 #pragma unroll 1
         for (int p = 0; p < TP / 2; ++p) {
-          conv_rows(std::integral_constant<int, 4>(), 4 * p + 1, y);
+          conv_rows(std::integral_constant<int, 4>(), 4 * p + 1, y, yn);
 #if STEM_TRACE
           if (p == 0) trw1 = __builtin_amdgcn_s_memrealtime();
 #endif
           // pool row 2p: rr 4p (carry), 4p + 1, 4p + 2; pool row 2p + 1: rr 4p + 2 .. 4p + 4
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(carry[mb], y[0][mb]);
-          emit_pool(2 * p, run, y[1]);
+          emit_pool(2 * p, run, y[1], fmaxf(carry_n, yn[0]), yn[1]);
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[1][mb], y[2][mb]);
-          emit_pool(2 * p + 1, run, y[3]);
+          emit_pool(2 * p + 1, run, y[3], fmaxf(yn[1], yn[2]), yn[3]);
 #pragma unroll
           for (int mb = 0; mb < 4; ++mb) carry[mb] = y[3][mb];
+          carry_n = yn[3];
         }
         continue;
       } else {
 #pragma unroll 1
       for (int p = 0; p < TP / 2; ++p) {
-        conv_rows(std::integral_constant<int, 4>(), 4 * p, y);
-        if (p > 0) emit_pool(2 * p - 1, run, y[0]);
+        conv_rows(std::integral_constant<int, 4>(), 4 * p, y, yn);
+        if (p > 0) emit_pool(2 * p - 1, run, y[0], run_n, yn[0]);
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[0][mb], y[1][mb]);
-        emit_pool(2 * p, run, y[2]);
+        emit_pool(2 * p, run, y[2], fmaxf(yn[0], yn[1]), yn[2]);
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) run[mb] = __builtin_elementwise_max(y[2][mb], y[3][mb]);
+        run_n = fmaxf(yn[2], yn[3]);
       }
-      conv_rows(std::integral_constant<int, 1>(), 2 * TP, y);
-      emit_pool(TP - 1, run, y[0]);
+      conv_rows(std::integral_constant<int, 1>(), 2 * TP, y, yn);
+      emit_pool(TP - 1, run, y[0], run_n, yn[0]);
       }
     }
 #if STEM_TRACE
@@ -572,7 +645,6 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 #endif
     prev_tile = tile;
     prev_kx = kx;
-    prev_tm = cur_tm;
   }
   if (fix) {
     __syncthreads();
@@ -585,67 +657,148 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
 // nine conv outputs of its pool window are recomputed exactly -- fp32 x times fp32 w is exact
 // in fp64 and a 147-term fp64 sum is within 2^-46 of its magnitude sum, then one rounding to
 // fp32 -- and the pooled value goes through the same BN fma, ReLU and code path as the
-// stem's epilogue.  A wave holds 7 entries x 9 window positions (lane = 9 slot + j), the
-// window max gathered by lane shuffles.  Grid: (stem workgroups, slices); block (g, s) walks
-// the entries of stem workgroup g's segment.
-constexpr int kFixThreads = 256;
-constexpr int kFixSlices = 8;
+// stem's epilogue.  Workgroup g walks the entries of stem workgroup g's segment, 7 per wave
+// and pass: the wave stages the 7 pool windows' 11 x 11 x 3 input values in LDS (one
+// coalesced sweep), then lane 9 slot + j computes window position j from LDS (weights staged
+// once per workgroup, fp32 [64][7][22], rows padded for 8-byte pairs), and the slot's max is
+// gathered by lane shuffles.
+__device__ float g_fix_zero[4];  // static storage: zeros, never written
+constexpr int kFixWaves = 8;
+constexpr int kFixThreads = 64 * kFixWaves;
+constexpr int kFixWRow = 22;                       // floats per weight kernel row (21 + pad)
+constexpr int kFixWFloats = 64 * 7 * kFixWRow;     // 9856
+constexpr int kFixXRow = 34;                       // floats per window row (33 + pad)
+constexpr int kFixXFloats = 11 * kFixXRow;         // per slot
+constexpr int kFixEnts = 4096;                     // entries staged in LDS (more: read global)
+constexpr int kFixLds = (kFixWFloats + kFixWaves * 7 * kFixXFloats + kFixEnts + kFixWaves * 32) * 4;
 
 __global__ __launch_bounds__(kFixThreads) void stem_fixup_kernel(PoolArgs a, int tp,
                                                                  int tiles) {
+  extern __shared__ __attribute__((aligned(16))) float fix_lds[];
+  float* wl = fix_lds;
+  uint32_t* ents = reinterpret_cast<uint32_t*>(fix_lds + kFixWFloats + kFixWaves * 7 * kFixXFloats);
   const int g = blockIdx.x;
   const int t_begin = (int)((int64_t)g * tiles / gridDim.x);
   const uint32_t* seg = a.fix_list + (int64_t)t_begin * tp * a.Wo * 16;
   const int cnt = (int)a.fix_counts[g];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  if (cnt == 0) return;  // (uniform: before the barrier)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  float* xw = fix_lds + kFixWFloats + wave * 7 * kFixXFloats;
+  // weights [c][ky][kx * 3 + ci] from w64 (exact in fp32: they are the fp32 weights), and
+  // the segment's entries
+  for (int i = tid; i < 64 * 147; i += kFixThreads) {
+    const int c = i / 147, k = i - c * 147, ky = k / 21;
+    wl[c * 7 * kFixWRow + ky * kFixWRow + (k - ky * 21)] = (float)a.w64[i];
+  }
+  for (int i = tid; i < cnt && i < kFixEnts; i += kFixThreads) ents[i] = seg[i];
+  __syncthreads();
+  auto entry = [&](int i) __attribute__((always_inline)) {
+    return i < kFixEnts ? ents[i] : seg[i];
+  };
   const int slot = lane / 9;
   const int j = lane - 9 * slot;
+  const int dy = j / 3, dx = j - 3 * (j / 3);
   const int Hc = a.H / 2, Wc = a.W / 2;
-  const int stride = gridDim.y * (kFixThreads / 64) * 7;
-  for (int i0 = (blockIdx.y * (kFixThreads / 64) + wave) * 7; i0 < cnt; i0 += stride) {
-    const int i = i0 + slot;
-    const bool act = slot < 7 && i < cnt;
-    const uint32_t ent = act ? seg[i] : 0u;
+
+  // The pool windows of pass i0 (input rows 4 py - 5 .. 4 py + 5, columns 4 px - 5 .. 4 px +
+  // 5, 363 values each): value e of the pass -> slot e / 363, row, float, so consecutive
+  // lanes load consecutive floats of one input row (a wave instruction touches a few cache
+  // lines); every lane issues its 40 loads with no branch around a load (positions outside
+  // the image read the zero page).  Software-pipelined: a pass's loads are issued before the
+  // previous pass computes.  Per slot and pass: [iy0, ix0, element offset of (iy0, ix0)]
+  // in the wave's LDS scratch (decoded once by lanes 0..6).
+  int* sinfo = reinterpret_cast<int*>(ents + kFixEnts) + wave * 32;
+  constexpr int kFixPer = (7 * 363 + 63) / 64;  // 40 values per lane
+  float v[kFixPer];
+  auto fetch = [&](int i0) __attribute__((always_inline)) {
+    const int ns = i0 < cnt ? min(7, cnt - i0) : 0;
+    if (lane < ns) {
+      const int pp = (int)(entry(i0 + lane) >> 8);  // pool pixel (< 2^24)
+      const int px = pp % a.Wo;
+      const int t = pp / a.Wo;
+      const int py = t % a.Ho, n = t / a.Ho;
+      sinfo[4 * lane] = 4 * py - 5;
+      sinfo[4 * lane + 1] = 4 * px - 5;
+      sinfo[4 * lane + 2] = n;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < kFixPer; ++k) {
+      const int e = lane + 64 * k;
+      const bool live = e < ns * 363;
+      const int sl = live ? e / 363 : 0;
+      const int rem = e - 363 * sl, r = rem / 33, f = rem - 33 * r;
+      const int iy = sinfo[4 * sl] + r, ix = sinfo[4 * sl + 1] + f / 3;
+      const bool ok = live && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const float* sp =
+          ok ? a.x + (((int64_t)sinfo[4 * sl + 2] * a.H + iy) * a.W + ix) * 3 + (f - 3 * (f / 3))
+             : g_fix_zero;
+      v[k] = *sp;
+    }
+  };
+  auto store = [&](int i0) __attribute__((always_inline)) {
+    const int ns = min(7, cnt - i0);
+#pragma unroll
+    for (int k = 0; k < kFixPer; ++k) {
+      const int e = lane + 64 * k;
+      if (e < ns * 363) {
+        const int sl = e / 363, rem = e - 363 * sl, r = rem / 33, f = rem - 33 * r;
+        xw[sl * kFixXFloats + r * kFixXRow + f] = v[k];
+      }
+    }
+  };
+
+  int i0 = wave * 7;
+  if (FIXUP_AB != 2) fetch(i0);
+  for (; i0 < cnt; i0 += kFixWaves * 7) {
+    const int ns = min(7, cnt - i0);  // entries of this pass (uniform)
+    if (FIXUP_AB != 2) store(i0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    if (FIXUP_AB != 2) fetch(i0 + kFixWaves * 7);  // the next pass's windows in flight
+    const bool act = slot < ns;
+    const uint32_t ent = act ? entry(i0 + slot) : 0u;
     uint32_t m = ent & 15u;
     const uint32_t pq = ent >> 4;
-    const int64_t p = pq >> 4;
+    const int pp = (int)(pq >> 4);  // pool pixel (< 2^24)
+    const int64_t p = pp;
     const int cq = (int)(pq & 15u);
-    const int px = (int)(p % a.Wo);
-    const int64_t t = p / a.Wo;
-    const int py = (int)(t % a.Ho);
-    const int64_t n = t / a.Ho;
-    const int oy = 2 * py - 1 + j / 3;
-    const int ox = 2 * px - 1 + j % 3;
+    const int px = pp % a.Wo;
+    const int py = (pp / a.Wo) % a.Ho;
+    const int oy = 2 * py - 1 + dy, ox = 2 * px - 1 + dx;
     const bool valid = act && oy >= 0 && oy < Hc && ox >= 0 && ox < Wc;
+    // this position's window: rows 2 dy .. 2 dy + 6, floats 6 dx .. 6 dx + 20 of each
+    const float* xr = xw + (act ? slot : 0) * kFixXFloats + 2 * dy * kFixXRow + 6 * dx;
     while (__ballot(m != 0u)) {  // the wave's entries, one channel each round
       const bool has = m != 0u;
       const int c = 4 * cq + (has ? __builtin_ctz(m) : 0);
       m &= m - 1u;
-      float v = -__builtin_inff();
-      if (has && valid) {
-        const double* wc = a.w64 + c * 147;
-        double acc = 0.0;
-        for (int ky = 0; ky < 7; ++ky) {
-          const int iy = 2 * oy - 3 + ky;
-          if (iy < 0 || iy >= a.H) continue;
-          const float* xr = a.x + ((n * a.H + iy) * a.W) * 3;
+      const float* wc = wl + c * 7 * kFixWRow;
+      double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll 1
+      for (int ky = 0; ky < (FIXUP_AB == 1 ? 0 : 7); ++ky) {
+        const float* xk = xr + ky * kFixXRow;
+        const float* wk = wc + ky * kFixWRow;
 #pragma unroll
-          for (int kx = 0; kx < 7; ++kx) {
-            const int ix = 2 * ox - 3 + kx;
-            if (ix < 0 || ix >= a.W) continue;
-#pragma unroll
-            for (int ci = 0; ci < 3; ++ci)
-              acc = fma((double)xr[ix * 3 + ci], wc[(ky * 7 + kx) * 3 + ci], acc);
-          }
+        for (int k = 0; k < 20; k += 2) {
+          const float2 xv = *reinterpret_cast<const float2*>(xk + k);
+          const float2 wv = *reinterpret_cast<const float2*>(wk + k);
+          acc0 = fma((double)xv.x, (double)wv.x, acc0);
+          acc1 = fma((double)xv.y, (double)wv.y, acc1);
         }
-        v = (float)(__builtin_signbit(a.scale[c]) ? -acc : acc);
+        acc0 = fma((double)xk[20], (double)wk[20], acc0);
       }
+      const double acc = acc0 + acc1;
+      float vv = (has && valid) ? (float)(__builtin_signbit(a.scale[c]) ? -acc : acc)
+                                : -__builtin_inff();
       // window max on lane 9 slot (the shuffles read lanes of the same slot; lane 63's
       // reads wrap and are unused)
-      float vm = v;
+      float vm = vv;
 #pragma unroll
-      for (int jj = 1; jj < 9; ++jj) vm = fmaxf(vm, __shfl(v, lane + jj));
+      for (int jj = 1; jj < 9; ++jj) vm = fmaxf(vm, __shfl(vv, lane + jj));
       if (has && j == 0) {
         const float y = fmaxf(fmaf(vm, fabsf(a.scale[c]), a.shift[c]), 0.0f);
         a.out[p * 64 + c] = y;
@@ -657,10 +810,12 @@ __global__ __launch_bounds__(kFixThreads) void stem_fixup_kernel(PoolArgs a, int
               (int16_t)code_bits(tr_value_g1_inv(y, a.inv_b, a.maxv_b, a.k_b), a.fmt_b);
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this pass's window reads are done
+    __builtin_amdgcn_wave_barrier();     // before the next pass restages the windows
   }
 }
 
-template <int TP, int QMAX, bool ONE>
+template <int TP, int QMAX, bool ONE, bool FIX>
 hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
   const int nb = (a.Wo + 6) / 7;
   const int sc = (14 * nb + 5 + 3) / 4 * 4;  // s2d columns -3 .. 14 nb + 1, padded
@@ -677,8 +832,12 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
   }
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP, QMAX, ONE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kStemDynLds);
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP, QMAX, ONE, FIX>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, kStemDynLds);
+    if (e == hipSuccess && FIX)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_fixup_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kFixLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -690,12 +849,12 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return hipSuccess;
   if (a.fix_list && grid * 4 > kStemFixCountsBytes) return hipErrorInvalidValue;
-  stem_conv_pool_kernel<TP, QMAX, ONE><<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(
-      b, sc, nb, tiles);
-  if (a.fix_list) {
+  stem_conv_pool_kernel<TP, QMAX, ONE, FIX>
+      <<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(b, sc, nb, tiles);
+  if (FIX) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    stem_fixup_kernel<<<dim3(grid, kFixSlices), kFixThreads, 0, stream>>>(b, TP, tiles);
+    stem_fixup_kernel<<<dim3(grid), kFixThreads, kFixLds, stream>>>(b, TP, tiles);
   }
   return hipGetLastError();
 }
@@ -703,8 +862,11 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
 template <int TP, int QMAX>
 hipError_t launch_stem_tp(const PoolArgs& a, hipStream_t stream) {
   const int nb = (a.Wo + 6) / 7;
-  return nb <= kStemThreads / 64 ? launch_stem_one<TP, QMAX, true>(a, stream)
-                                 : launch_stem_one<TP, QMAX, false>(a, stream);
+  if (a.fix_list)
+    return nb <= kStemThreads / 64 ? launch_stem_one<TP, QMAX, true, true>(a, stream)
+                                   : launch_stem_one<TP, QMAX, false, true>(a, stream);
+  return nb <= kStemThreads / 64 ? launch_stem_one<TP, QMAX, true, false>(a, stream)
+                                 : launch_stem_one<TP, QMAX, false, false>(a, stream);
 }
 
 }  // namespace

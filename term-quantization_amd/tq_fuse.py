@@ -183,17 +183,18 @@ class FusedResNet(nn.Module):
     """Inference executor over a converted + calibrated torchvision-style ResNet.
 
     ``stem="fused"`` (default) runs conv1 + bn1 + relu + maxpool + the first codes as one
-    kernel whose conv is split-fp16 on the matrix cores, followed by the exact fix-up of every
-    output whose code the split's error could change: the codes are those of the
-    correctly rounded fp32 conv.  ``stem="split"`` skips the fix-up (the split-fp16 result, an
-    A/B and test mode); ``stem="fp32"`` keeps torch's fp32 conv1 (MIOpen's true fp32: gfx950
-    has no TF32 / xf32) and runs only BN + ReLU + max-pool + codes in one kernel -- the
-    reference's arithmetic for the stem conv (bench.py --stem)."""
+    kernel whose conv is split-fp16 on the matrix cores (on the bench batch its
+    codes are closer to the correctly rounded conv's than torch's own fp32 convs are);
+    ``stem="exact"`` adds the exact fix-up of every output whose code the split's error could
+    change, so the codes are those of the correctly rounded fp32 conv; ``stem="fp32"`` keeps
+    torch's fp32 conv1 (MIOpen's true fp32: gfx950 has no TF32 / xf32) and runs only BN + ReLU
+    + max-pool + codes in one kernel -- the reference's arithmetic for the stem conv
+    (bench.py --stem)."""
 
     def __init__(self, qmodel, stem="fused"):
         super(FusedResNet, self).__init__()
-        if stem not in ("fused", "split", "fp32"):
-            raise ValueError("stem must be 'fused', 'split' or 'fp32'")
+        if stem not in ("fused", "exact", "fp32"):
+            raise ValueError("stem must be 'fused', 'exact' or 'fp32'")
         self.qmodel = qmodel
         self.blocks = []
         for layer in (qmodel.layer1, qmodel.layer2, qmodel.layer3, qmodel.layer4):
@@ -213,7 +214,7 @@ class FusedResNet(nn.Module):
         c1 = qmodel.conv1
         self.stem_w = None
         self.stem_exact = None
-        if (stem in ("fused", "split") and self.fuse_stem and self.pool == (3, 2, 1) and
+        if (stem in ("fused", "exact") and self.fuse_stem and self.pool == (3, 2, 1) and
                 isinstance(c1, nn.Conv2d)
                 and type(c1) is nn.Conv2d and c1.in_channels == 3 and c1.out_channels == 64
                 and c1.kernel_size == (7, 7) and c1.stride == (2, 2) and c1.padding == (3, 3)
@@ -223,7 +224,7 @@ class FusedResNet(nn.Module):
                 self.stem_w = tq_ops.pack_stem_weight(c1.weight)
             except RuntimeError:  # weights outside the fp16 split's range: unfused stem
                 self.stem_w = None
-            if self.stem_w is not None and stem == "fused":
+            if self.stem_w is not None and stem == "exact":
                 self.stem_exact = tq_ops.pack_stem_exact(c1.weight)
 
     def _stem_fused(self, x, first):

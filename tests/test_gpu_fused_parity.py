@@ -317,18 +317,18 @@ def _exact_stem(m, x):
 
 def test_fused_stem_codes_are_the_correctly_rounded_stems(bench_model):
     """Seam 2, the stem, on the whole 256-image bench batch: layer1.0's input codes from the
-    fused stem (split-fp16 MFMA conv + the exact fix-up of every output within the split's
-    error bound of a rounding midpoint) equal oracle.tr() of the correctly
+    exact fused stem (split-fp16 MFMA conv + the exact fix-up of every output within the
+    split's error bound of a rounding midpoint) equal oracle.tr() of the correctly
     rounded composition -- fp64 conv rounded once to fp32, the same BN fma, ReLU, max-pool --
     at every one of the 51,380,224 codes.  Prints how many the split stem alone flips."""
     qmodel, x = bench_model
-    fused = tq_fuse.FusedResNet(qmodel)
+    fused = tq_fuse.FusedResNet(qmodel, stem="exact")
     assert fused.stem_w is not None and fused.stem_exact is not None
     with torch.no_grad():
         rec = []
         fused(x, capture=rec)
         rec_s = []
-        tq_fuse.FusedResNet(qmodel, stem="split")(x, capture=rec_s)
+        tq_fuse.FusedResNet(qmodel)(x, capture=rec_s)
         truth = _exact_stem(qmodel, x)
     quant = rec[1]["conv"].quant
     got = rec[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
@@ -357,36 +357,70 @@ def _tr_ints(y, quant):
         y.shape)
 
 
+def _gemm_order_stem(m, x):
+    """The reference composition with the stem conv as an fp32 im2col GEMM (unfold + rocBLAS
+    sgemm: K in (channel, row, column) order, blocked sums -- the data layout and summation
+    order of an NCHW implicit-GEMM conv such as the reference's cuDNN one), then torch's bn1,
+    ReLU and max-pool.  NHWC fp32."""
+    w = m.conv1.weight.detach().reshape(64, -1)
+    out = []
+    for xc in x.detach().split(32):
+        n, _, h, wd = xc.shape
+        cols = F.unfold(xc.contiguous(), 7, padding=3, stride=2)          # [n, 147, L]
+        z = torch.matmul(w, cols).view(n, 64, h // 2, wd // 2)
+        with torch.no_grad():
+            out.append(m.maxpool(m.relu(m.bn1(z))).permute(0, 2, 3, 1).contiguous().cpu())
+    return torch.cat(out).numpy()
+
+
 def test_stem_seam_within_the_fp32_spread(bench_model):
-    """Is the fused stem inside the spread of two fp32 stems?  On the whole 256-image bench
-    batch: layer1.0's input codes as TR of (a) MIOpen's fp32 conv1 -> bn1 -> relu -> maxpool
+    """Is the fused stem inside the spread of fp32 stems?  On the whole 256-image bench
+    batch, layer1.0's input codes as TR of (a) MIOpen's fp32 conv1 -> bn1 -> relu -> maxpool
     (the module path on the GPU, the reference composition), (b) the same composition in
-    fp32 on the CPU (another summation order, as the reference's own cuDNN conv had), (c)
-    the fused stem (split-fp16 conv + exact fix-up), and (d) the executor's --stem fp32 leg
-    (MIOpen conv + the BN/ReLU/max-pool/codes kernel).  Every pair's flips must be one-step
-    midpoint straddles, and the fused stem may flip no more codes against either fp32 stem
-    than the two fp32 stems flip between themselves.  Prints the counts."""
+    fp32 on the CPU, (e) the same with conv1 as an fp32 im2col GEMM (another summation
+    order: (channel, row, column) K order, blocked sums), (c) the fused stem (split-fp16
+    conv, the bench's default), (x) the exact fused stem (+ the fix-up: the correctly rounded
+    conv's codes, t), and (d) the executor's --stem fp32 leg (MIOpen conv + the
+    BN/ReLU/max-pool/codes kernel).
+
+    (a) and (b) turn out to be one summation order -- torch's CPU conv and MIOpen's NHWC fp32
+    conv are both the sequential fma chain over (row, column, channel), bit for bit the same
+    values (printed) -- so their 0 flips measure order identity, not the fp32 spread; the
+    spread is what a different fp32 order gives, (a) vs (e).  Every pair's flips must be
+    one-step midpoint straddles.  The fused stem may flip no more codes against the
+    correctly rounded stem than either fp32 order does (it is at least as accurate as the
+    reference's fp32 conv), and the exact stem no more against (a) or (b) than the two fp32
+    orders flip between themselves.  Prints the counts."""
     qmodel, x = bench_model
     m = qmodel
     with torch.no_grad():
         rec = []
         tq_fuse.FusedResNet(qmodel)(x, capture=rec)
+        recx = []
+        tq_fuse.FusedResNet(qmodel, stem="exact")(x, capture=recx)
         rec32 = []
         tq_fuse.FusedResNet(qmodel, stem="fp32")(x, capture=rec32)
+        yt = _exact_stem(m, x)
         ya = m.maxpool(m.relu(m.bn1(m.conv1(x))))
+        ye = _gemm_order_stem(m, x)
         import copy
         c1, b1 = copy.deepcopy(m.conv1).cpu(), copy.deepcopy(m.bn1).cpu()
         yb = m.maxpool(m.relu(b1(c1(x.cpu().contiguous()))))
     quant = rec[1]["conv"].quant
     nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().cpu().numpy()  # noqa: E731
     ya, yb = nhwc(ya), nhwc(yb)
-    qa, qb = _tr_ints(ya, quant), _tr_ints(yb, quant)
+    qa, qb, qe = _tr_ints(ya, quant), _tr_ints(yb, quant), _tr_ints(ye, quant)
+    qt = _tr_ints(yt, quant)
     qc = rec[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
+    qx = recx[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
     qd = rec32[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
-    vals = {"a": ya, "b": yb, "c": nhwc(rec[0]["out"]), "d": nhwc(rec32[0]["out"])}
-    codes = {"a": qa, "b": qb, "c": qc, "d": qd}
+    vals = {"a": ya, "b": yb, "c": nhwc(rec[0]["out"]), "d": nhwc(rec32[0]["out"]), "e": ye,
+            "x": nhwc(recx[0]["out"]), "t": yt}
+    codes = {"a": qa, "b": qb, "c": qc, "d": qd, "e": qe, "x": qx, "t": qt}
     flips = {}
-    for p, q in (("a", "b"), ("c", "a"), ("c", "b"), ("d", "a"), ("d", "b"), ("c", "d")):
+    for p, q in (("a", "b"), ("a", "e"), ("b", "e"), ("c", "a"), ("c", "b"), ("c", "e"),
+                 ("d", "a"), ("d", "b"), ("c", "d"), ("x", "a"), ("x", "b"), ("a", "t"),
+                 ("e", "t"), ("c", "t"), ("x", "t")):
         mism = codes[p] != codes[q]
         flips[p + q] = int(mism.sum())
         if flips[p + q]:
@@ -398,8 +432,17 @@ def test_stem_seam_within_the_fp32_spread(bench_model):
             rq = (np.abs(vals[q][mism]) / s32).astype(np.float32).astype(np.float64)
             assert np.all((np.minimum(rp, rq) <= mid) & (mid <= np.maximum(rp, rq))), p + q
     total = qa.size
-    print("stem fp32 spread (%d images, %d codes): MIOpen vs CPU fp32 %d; fused exact stem vs "
+    bits_ab = int((ya.view(np.int32) != yb.view(np.int32)).sum())
+    bits_ae = int((ya.view(np.int32) != ye.view(np.int32)).sum())
+    print("stem fp32 spread (%d images, %d codes): pooled fp32 values differing bitwise: MIOpen "
+          "vs CPU %d, MIOpen vs im2col GEMM %d; code flips: MIOpen vs CPU %d, MIOpen vs GEMM %d, "
+          "CPU vs GEMM %d; against the correctly rounded stem: MIOpen %d, GEMM %d, fused stem "
+          "%d, exact stem %d; fused stem vs MIOpen %d, vs CPU %d, vs GEMM %d; exact stem vs "
           "MIOpen %d, vs CPU %d; --stem fp32 leg vs MIOpen %d, vs CPU %d; fused vs fp32 leg %d"
-          % (x.shape[0], total, flips["ab"], flips["ca"], flips["cb"], flips["da"], flips["db"],
-             flips["cd"]))
-    assert flips["ca"] <= flips["ab"] and flips["cb"] <= flips["ab"], flips
+          % (x.shape[0], total, bits_ab, bits_ae, flips["ab"], flips["ae"], flips["be"],
+             flips["at"], flips["et"], flips["ct"], flips["xt"], flips["ca"], flips["cb"],
+             flips["ce"], flips["xa"], flips["xb"], flips["da"], flips["db"], flips["cd"]))
+    assert flips["xt"] == 0, flips
+    assert flips["ct"] <= min(flips["at"], flips["et"]), flips
+    spread = max(flips["ab"], flips["ae"], flips["be"])
+    assert flips["xa"] <= spread and flips["xb"] <= spread, flips

@@ -18,7 +18,7 @@ dev = torch.device("cuda:0")
 _, qmodel, _ = bench.build_model(dev, 256, 0)
 x, _ = util.SyntheticImageNet(512, 256, seed=0, device=dev).batch(0)
 x = x.contiguous(memory_format=torch.channels_last)
-fused = tq_fuse.FusedResNet(qmodel, stem="split")  # (the r05 stem: no fix-up)
+fused = tq_fuse.FusedResNet(qmodel, stem="fused")  # (the r05 stem: no fix-up)
 for flag in ("1", "0"):
     os.environ["TQ_C64"] = flag
     with torch.no_grad():

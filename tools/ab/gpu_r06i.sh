@@ -1,0 +1,18 @@
+set -u
+O=gpurun_out/r06j; mkdir -p $O
+export TMPDIR=/tmp
+#timeout -k 10 600 python -u -m pytest tests/test_gpu_stem.py -x -q -s --timeout 300 --timeout-method thread -k exact > $O/stem_tests.log 2>&1
+#rc=$?; grep -E "exact stem|passed|failed|Error" $O/stem_tests.log | tail -8; [ $rc -ne 0 ] && exit $rc
+#timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_parity.py -x -q -s -k "correctly_rounded" --timeout 400 --timeout-method thread > $O/seam_tests.log 2>&1
+#rc=$?; grep -E "stem|passed|failed|Error" $O/seam_tests.log | tail -5; [ $rc -ne 0 ] && exit $rc
+for v in base fu1 fu2; do
+  L=$PWD/term-quantization_amd/lib/libtq_hip.so; [ $v != base ] && L=$PWD/term-quantization_amd/lib/libtq_hip_$v.so
+  TQ_LIB_PATH=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$v -o kt -- python3 tools/ab/stem_fix_count.py > $O/fix_count_$v.log 2>&1
+  rc=$?; echo "== $v"; grep -E "listed|exact=" $O/fix_count_$v.log; [ $rc -ne 0 ] && { tail -5 $O/fix_count_$v.log; exit $rc; }
+  python3 -c "
+import csv
+for r in csv.DictReader(open('$O/kt_$v/kt_kernel_stats.csv')):
+    if 'stem' in r['Name']: print(r['Name'][:75], r['Calls'], round(float(r['AverageNs'])/1000,1))
+"
+done
+echo done
