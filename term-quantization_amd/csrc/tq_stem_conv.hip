@@ -63,6 +63,11 @@
 #ifndef STEM_NRM_MFMA
 #define STEM_NRM_MFMA 1  // window norms: 1 the diagonal of an MFMA, 0 v_dot2 on the VALU
 #endif
+#ifndef STEM_QF32
+#define STEM_QF32 0  // 1: the code-table index from an fp32 product (exact fp64 quotient only
+                     // near a rounding midpoint); 0: every quotient in fp64 (r06: the fp32
+                     // form made the stem 12-18 us slower in the bench, profiles/r06_stem_q_ab.txt)
+#endif
 #ifndef FIXUP_AB
 #define FIXUP_AB 0  // timing-only builds of the fix-up kernel: 1 no sums, 2 no window staging
 #endif
@@ -104,6 +109,19 @@ __device__ __forceinline__ float row_down(float v) {
 
 // ONE: one strip per wave (nb <= 8 waves: Wo <= 56), the strip's last conv row carried to
 // the next tile (STEM_CARRY)
+// relu_q (tq_device.h: q = round(fp32(y / sf)), y >= 0, clamped to maxv) from an fp32
+// product y * fp32(1 / sf): |r_fast - fp32(y / sf)| <= 3 * 2^-24 r, so the rounded integer
+// can differ only when r_fast lies within that of a half-integer; those values (about one in
+// 4000) take the exact fp64 quotient (as tq_device.h's TQ_EPI_F32 relu_q_epi)
+__device__ __forceinline__ uint32_t stem_relu_q(float y, double inv_sf, float maxv) {
+  if (!STEM_QF32) return relu_q(y, inv_sf, maxv);
+  const float r = fminf(y * (float)inv_sf, maxv + 1.0f);
+  const float fr = __builtin_amdgcn_fractf(r);
+  if (__builtin_expect(fabsf(fr - 0.5f) <= r * 0x1p-21f, 0)) return relu_q(y, inv_sf, maxv);
+  const uint32_t q = (uint32_t)r + (fr >= 0.5f ? 1u : 0u);
+  return q < (uint32_t)maxv ? q : (uint32_t)maxv;
+}
+
 // sum of squares of an 8-value fp16 slice, added to acc (v_dot2_f32_f16)
 __device__ __forceinline__ float sq8(const f16x8& v, float acc) {
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -532,7 +550,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
             }
             if (lut) {  // the fast path's codes from the LDS table
 #pragma unroll
-              for (int i = 0; i < 4; ++i) v[i] = lut[relu_q(yv[i], inv, maxv)];
+              for (int i = 0; i < 4; ++i) v[i] = lut[stem_relu_q(yv[i], inv, maxv)];
             } else if (inv > 0.0 && inv <= 1.0e308) {  // yv >= 0 (ReLU, max), 0 < sf < inf
               int32_t t[4];
               tr_values_relu4(yv, inv, maxv, relu_peels(maxv, k), t);
