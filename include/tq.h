@@ -390,15 +390,6 @@ int tq_stem_conv_pool_encode(const float *x, int64_t n, int64_t h, int64_t w,
 int64_t tq_stem_workspace_bytes(int64_t n, int64_t h, int64_t w);
 
 /*
- * Classifier head of the fused ResNet executor: out = fc(avgpool(x)) (torchvision
- * ResNet.forward's avgpool -> flatten -> fc, both fp32 torch in the reference -- not TQ
- * layers).  x fp32 channels_last [n][hw][c] (16-byte aligned, c % 4 == 0), w fp32
- * [o][c], b fp32 [o] or NULL, pooled fp32 [n][c] scratch, out fp32 [n][o].
- */
-int tq_avgpool_fc_f32(const float *x, int64_t n, int64_t hw, int64_t c, const float *w,
-                      const float *b, int64_t o, float *pooled, float *out, void *stream);
-
-/*
  * Batched activation-scale calibration, replacing the 2048-launch loop of
  * tr_layer.mse_profile (tr_layer.py:43-54):
  *   errs[s] = sum_b hist[b] * (x[b] - TR(x[b]; sf = sfs[s], bitwidth, group 1, k))^2

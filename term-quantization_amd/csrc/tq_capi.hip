@@ -682,19 +682,6 @@ int tq_stem_conv_pool_encode(const float* x, int64_t n, int64_t h, int64_t w,
   return hip_status(e, "stem_conv_pool launch");
 }
 
-int tq_avgpool_fc_f32(const float* x, int64_t n, int64_t hw, int64_t c, const float* w,
-                      const float* b, int64_t o, float* pooled, float* out, void* stream) {
-  if (n < 0 || hw < 1 || c < 4 || c % 4 || o < 0 || n > (1 << 30) || o > (1 << 30) ||
-      hw > (1 << 20) || c > (1 << 20))
-    return fail(TQ_ERR_INVALID_ARGUMENT, "avgpool_fc: needs C >= 4, C % 4 == 0");
-  if (!x || !w || !pooled || !out || (uintptr_t)x % 16 || (uintptr_t)w % 16 ||
-      (uintptr_t)pooled % 16)
-    return fail(TQ_ERR_INVALID_ARGUMENT, "avgpool_fc: null or misaligned buffer");
-  return hip_status(tq::launch_avgpool_fc(x, n, hw, c, w, b, o, pooled, out,
-                                          (hipStream_t)stream),
-                    "avgpool_fc launch");
-}
-
 int tq_mse_profile(const float* x, const float* hist, int64_t nbins, const float* sfs,
                    int64_t nsf, int32_t bitwidth, int32_t num_keep_terms, double* errs,
                    void* stream) {

@@ -153,12 +153,6 @@ struct PoolArgs {
 constexpr int64_t kStemFixCountsBytes = 4096;
 
 hipError_t launch_bn_relu_maxpool_encode(const PoolArgs& a, hipStream_t stream);
-
-// classifier head (tq_head.hip): out = fc(avgpool(x)), x channels_last [N][HW][C] fp32,
-// w [O][C], b [O] or nullptr; pooled [N][C] scratch
-hipError_t launch_avgpool_fc(const float* x, int64_t N, int64_t HW, int64_t C, const float* w,
-                             const float* b, int64_t O, float* pooled, float* out,
-                             hipStream_t stream);
 hipError_t launch_stem_conv_pool(const PoolArgs& a, hipStream_t stream);
 
 // Squeeze-excite gate (tq_se.hip): gate = sigmoid(expand(swish(reduce(x_sq)))), both 1x1

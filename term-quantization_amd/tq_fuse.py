@@ -212,16 +212,6 @@ class FusedResNet(nn.Module):
         # the whole stem (conv + BN + ReLU + pool + codes) in one kernel when it is the
         # torchvision shape: conv 7x7/2 pad 3, 3 -> 64, no bias; pool 3x3/2 pad 1
         c1 = qmodel.conv1
-        # the head as one fused pooling + Linear pass when it is torchvision's
-        # AdaptiveAvgPool2d(1) -> flatten -> fp32 Linear
-        fc = getattr(qmodel, "fc", None)
-        ap = getattr(qmodel, "avgpool", None)
-        # (TQ_HEAD=0: torch's avgpool + fc, an A/B switch)
-        self.head_fused = (os.environ.get("TQ_HEAD", "1") != "0" and
-                           isinstance(fc, nn.Linear) and type(fc) is nn.Linear and
-                           fc.weight.dtype == torch.float32 and fc.in_features % 4 == 0 and
-                           isinstance(ap, nn.AdaptiveAvgPool2d) and
-                           ap.output_size in (1, (1, 1)))
         self.stem_w = None
         self.stem_exact = None
         if (stem in ("fused", "exact") and self.fuse_stem and self.pool == (3, 2, 1) and
@@ -399,12 +389,6 @@ class FusedResNet(nn.Module):
                 capture.append({"name": "block%d.conv2" % i, "conv": b.conv2, "codes_in": cin,
                                 "residual": identity, "out": x, "codes_a": codes,
                                 "codes_b": codes_down})
-        if self.head_fused and x.is_contiguous(memory_format=torch.channels_last):
-            # avgpool + flatten + fc in two short kernels (tq_avgpool_fc_f32)
-            result.append(tq_ops._launch(
-                "avgpool_fc", x.shape[0] * m.fc.out_features * m.fc.in_features,
-                lambda: tq_native.avgpool_fc(x, m.fc.weight, m.fc.bias)))
-            return
         x = m.avgpool(x)
         x = torch.flatten(x, 1)
         result.append(m.fc(x))

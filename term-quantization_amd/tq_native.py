@@ -101,7 +101,6 @@ _SIGNATURES["tq_stem_conv_pool_encode"] = [
     _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _f32, _i32, _i32, _i32,
     _vp, _i64, _f32, _i32, _i32, _i32, _vp, _vp, _vp, _i64, _vp]
 _SIGNATURES["tq_stem_workspace_bytes"] = [_i64, _i64, _i64]
-_SIGNATURES["tq_avgpool_fc_f32"] = [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp]
 _SIGNATURES["tq_conv2d_termpair_f16"] = [
     _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
     _i64, _f64, _vp, _vp, _i64, _i64, _i32, _i32, _i32, ctypes.POINTER(ConvEpilogue), _vp]
@@ -590,24 +589,6 @@ def stem_conv_pool_encode(x, w_split, scale, shift, out, codes_a=None, quant_a=N
             int(qb[1]), int(qb[2]), code_format(codes_b) if codes_b is not None else 0,
             _ptr(w64), _ptr(wbound), _ptr(workspace if exact is not None else None),
             workspace.numel() if (exact is not None) else 0, _stream(x))
-    _check(rc)
-    return out
-
-
-def avgpool_fc(x, weight, bias):
-    """fc(flatten(avgpool(x))) of a ResNet head (tq_avgpool_fc_f32): x fp32 channels_last
-    [N, C, H, W], weight fp32 [O, C], bias fp32 [O] or None -> [N, O]."""
-    n, c, h, w = x.shape
-    if not x.is_contiguous(memory_format=torch.channels_last):
-        raise RuntimeError("avgpool_fc: x must be channels_last contiguous")
-    weight = weight.contiguous()
-    o = weight.shape[0]
-    pooled = torch.empty((n, c), dtype=torch.float32, device=x.device)
-    out = torch.empty((n, o), dtype=torch.float32, device=x.device)
-    with torch.cuda.device(x.device):
-        rc = lib().tq_avgpool_fc_f32(_ptr(x), n, h * w, c, _ptr(weight),
-                                     _ptr(bias.contiguous() if bias is not None else None), o,
-                                     _ptr(pooled), _ptr(out), _stream(x))
     _check(rc)
     return out
 
