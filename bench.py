@@ -84,11 +84,11 @@ def parse(argv=None):
     ap.add_argument("--no-d4", action="store_true",
                     help="skip the d4 key (BASELINE configs[2]/[3]: LSTM-650, fused "
                          "MobileNet-V2 / EfficientNet-b0; rank 0 at N=1 only)")
-    ap.add_argument("--stem", choices=("fused", "exact", "fp32"), default="fused",
-                    help="fused: the fused stem kernel (split-fp16 near-fp32); exact: the "
-                         "fused stem kernel + its exact fix-up (codes of the correctly rounded "
-                         "fp32 conv); fp32: torch's fp32 conv + the BN/ReLU/max-pool/codes "
-                         "kernel")
+    ap.add_argument("--stem", choices=("fused", "exact", "fp32"), default="exact",
+                    help="exact: the fused stem kernel (split-fp16 MFMA conv) + its exact "
+                         "fix-up (the codes of the correctly rounded fp32 conv); fused: the "
+                         "fused stem kernel alone (near-fp32); fp32: torch's fp32 conv + the "
+                         "BN/ReLU/max-pool/codes kernel")
     ap.add_argument("--no-stem-leg", action="store_true",
                     help="skip the second timed pass with the other stem (N=1 only)")
     ap.add_argument("--unfused", action="store_true",
@@ -552,7 +552,8 @@ def main(argv=None):
 
         # the other stems: the same executor with the torch
         # fp32 stem conv (MIOpen, true fp32) + the BN/ReLU/max-pool/codes kernel, and with the
-        # fused stem's exact fix-up, timed the same way, reported beside the headline
+        # fused stem kernel with / without its exact fix-up, timed the same way, reported
+        # beside the headline
         stem_legs = {}
         if world == 1 and not args.unfused and not args.no_stem_leg:
             for other in ("fp32", "exact", "fused"):
@@ -717,8 +718,9 @@ def main(argv=None):
                                    "epilogue)",
                        "launch": launch, "streams": args.streams,
                        # the stem conv (not a TR layer; fp32 torch in the reference) runs in
-                       # the fused stem kernel as a split-fp16 near-fp32 conv,
-                       # or (--stem fp32) as torch's fp32 conv
+                       # the fused stem kernel as a split-fp16 conv with the exact fix-up
+                       # (default: correctly rounded codes), without it (--stem fused), or
+                       # (--stem fp32) as torch's fp32 conv
                        "stem": STEM_NAMES[args.stem if enc_name == "stem_conv_pool" else "fp32"]},
             "term_pair_macs_per_image": tmacs_per_img,
             "term_pair_macs_per_s": tmacs_per_img * ips,

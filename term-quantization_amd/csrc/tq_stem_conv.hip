@@ -69,7 +69,8 @@
                      // form made the stem 12-18 us slower in the bench, profiles/r06_stem_q_ab.txt)
 #endif
 #ifndef FIXUP_AB
-#define FIXUP_AB 0  // timing-only builds of the fix-up kernel: 1 no sums, 2 no window staging
+#define FIXUP_AB 0  // timing-only builds of the fix-up kernel: 1 no sums, 2 no window staging,
+                    // 3 the workgroup setup only
 #endif
 #ifndef STEM_FIXAB
 #define STEM_FIXAB 0  // timing-only builds of the fix-up listing: 1 no window norms, 2 no flags
@@ -712,6 +713,7 @@ __global__ __launch_bounds__(kFixThreads) void stem_fixup_kernel(PoolArgs a, int
   }
   for (int i = tid; i < cnt && i < kFixEnts; i += kFixThreads) ents[i] = seg[i];
   __syncthreads();
+  if (FIXUP_AB == 3) return;
   auto entry = [&](int i) __attribute__((always_inline)) {
     return i < kFixEnts ? ents[i] : seg[i];
   };

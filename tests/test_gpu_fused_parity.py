@@ -328,7 +328,7 @@ def test_fused_stem_codes_are_the_correctly_rounded_stems(bench_model):
         rec = []
         fused(x, capture=rec)
         rec_s = []
-        tq_fuse.FusedResNet(qmodel)(x, capture=rec_s)
+        tq_fuse.FusedResNet(qmodel, stem="fused")(x, capture=rec_s)
         truth = _exact_stem(qmodel, x)
     quant = rec[1]["conv"].quant
     got = rec[1]["codes_in"][..., :64].float().cpu().numpy().astype(np.int64)
@@ -395,7 +395,7 @@ def test_stem_seam_within_the_fp32_spread(bench_model):
     m = qmodel
     with torch.no_grad():
         rec = []
-        tq_fuse.FusedResNet(qmodel)(x, capture=rec)
+        tq_fuse.FusedResNet(qmodel, stem="fused")(x, capture=rec)
         recx = []
         tq_fuse.FusedResNet(qmodel, stem="exact")(x, capture=recx)
         rec32 = []
