@@ -72,6 +72,9 @@
 #define FIXUP_AB 0  // timing-only builds of the fix-up kernel: 1 no sums, 2 no window staging,
                     // 3 the workgroup setup only
 #endif
+#ifndef FIX_FUSED
+#define FIX_FUSED 1  // 1: the exact fix-up as the stem kernel's tail phase; 0: its own launch
+#endif
 #ifndef STEM_FIXAB
 #define STEM_FIXAB 0  // timing-only builds of the fix-up listing: 1 no window norms, 2 no flags
 #endif
@@ -133,6 +136,179 @@ __device__ __forceinline__ float sq8(const f16x8& v, float acc) {
   }
   return acc;
 }
+
+// Exact fix-up of the listed outputs (the FIX stem kernel's tail phase, FIX_FUSED; or one
+// launch after the stem, same stream).  Each entry
+// names a pool pixel p and a 4-bit mask of channels in quad cq; for each such channel the
+// nine conv outputs of its pool window are recomputed exactly -- fp32 x times fp32 w is exact
+// in fp64 and a 147-term fp64 sum is within 2^-46 of its magnitude sum, then one rounding to
+// fp32 -- and the pooled value goes through the same BN fma, ReLU and code path as the
+// stem's epilogue.  Workgroup g walks the entries of stem workgroup g's segment, 7 per wave
+// and pass: the wave stages the 7 pool windows' 11 x 11 x 3 input values in LDS (one
+// coalesced sweep), then lane 9 slot + j computes window position j from LDS (weights staged
+// once per workgroup, fp32 [64][7][22], rows padded for 8-byte pairs), and the slot's max is
+// gathered by lane shuffles.
+__device__ float g_fix_zero[4];  // static storage: zeros, never written
+constexpr int kFixWaves = 8;
+constexpr int kFixThreads = 64 * kFixWaves;
+constexpr int kFixWRow = 22;                       // floats per weight kernel row (21 + pad)
+constexpr int kFixWFloats = 64 * 7 * kFixWRow;     // 9856
+constexpr int kFixXRow = 34;                       // floats per window row (33 + pad)
+constexpr int kFixXFloats = 11 * kFixXRow;         // per slot
+constexpr int kFixEnts = 4096;                     // entries staged in LDS (more: read global)
+constexpr int kFixLds = (kFixWFloats + kFixWaves * 7 * kFixXFloats + kFixEnts + kFixWaves * 32) * 4;
+
+// one workgroup's segment (seg, cnt entries) with fix_lds >= kFixLds bytes of dynamic LDS:
+// the tail phase of the FIX stem kernel (FIX_FUSED) or the body of stem_fixup_kernel
+__device__ __forceinline__ void stem_fixup_run(const PoolArgs& a, const uint32_t* seg, int cnt,
+                                               float* fix_lds) {
+  float* wl = fix_lds;
+  uint32_t* ents = reinterpret_cast<uint32_t*>(fix_lds + kFixWFloats + kFixWaves * 7 * kFixXFloats);
+  if (cnt == 0) return;  // (uniform: before the barrier)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  float* xw = fix_lds + kFixWFloats + wave * 7 * kFixXFloats;
+  // weights [c][ky][kx * 3 + ci] from w64 (exact in fp32: they are the fp32 weights), and
+  // the segment's entries
+  for (int i = tid; i < 64 * 147; i += kFixThreads) {
+    const int c = i / 147, k = i - c * 147, ky = k / 21;
+    wl[c * 7 * kFixWRow + ky * kFixWRow + (k - ky * 21)] = (float)a.w64[i];
+  }
+  for (int i = tid; i < cnt && i < kFixEnts; i += kFixThreads) ents[i] = seg[i];
+  __syncthreads();
+  if (FIXUP_AB == 3) return;
+  auto entry = [&](int i) __attribute__((always_inline)) {
+    return i < kFixEnts ? ents[i] : seg[i];
+  };
+  const int slot = lane / 9;
+  const int j = lane - 9 * slot;
+  const int dy = j / 3, dx = j - 3 * (j / 3);
+  const int Hc = a.H / 2, Wc = a.W / 2;
+
+  // The pool windows of pass i0 (input rows 4 py - 5 .. 4 py + 5, columns 4 px - 5 .. 4 px +
+  // 5, 363 values each): value e of the pass -> slot e / 363, row, float, so consecutive
+  // lanes load consecutive floats of one input row (a wave instruction touches a few cache
+  // lines); every lane issues its 40 loads with no branch around a load (positions outside
+  // the image read the zero page).  Software-pipelined: a pass's loads are issued before the
+  // previous pass computes.  Per slot and pass: [iy0, ix0, element offset of (iy0, ix0)]
+  // in the wave's LDS scratch (decoded once by lanes 0..6).
+  int* sinfo = reinterpret_cast<int*>(ents + kFixEnts) + wave * 32;
+  constexpr int kFixPer = (7 * 363 + 63) / 64;  // 40 values per lane
+  float v[kFixPer];
+  auto fetch = [&](int i0) __attribute__((always_inline)) {
+    const int ns = i0 < cnt ? min(7, cnt - i0) : 0;
+    if (lane < ns) {
+      const int pp = (int)(entry(i0 + lane) >> 8);  // pool pixel (< 2^24)
+      const int px = pp % a.Wo;
+      const int t = pp / a.Wo;
+      const int py = t % a.Ho, n = t / a.Ho;
+      sinfo[4 * lane] = 4 * py - 5;
+      sinfo[4 * lane + 1] = 4 * px - 5;
+      sinfo[4 * lane + 2] = n;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < kFixPer; ++k) {
+      const int e = lane + 64 * k;
+      const bool live = e < ns * 363;
+      const int sl = live ? e / 363 : 0;
+      const int rem = e - 363 * sl, r = rem / 33, f = rem - 33 * r;
+      const int iy = sinfo[4 * sl] + r, ix = sinfo[4 * sl + 1] + f / 3;
+      const bool ok = live && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const float* sp =
+          ok ? a.x + (((int64_t)sinfo[4 * sl + 2] * a.H + iy) * a.W + ix) * 3 + (f - 3 * (f / 3))
+             : g_fix_zero;
+      v[k] = *sp;
+    }
+  };
+  auto store = [&](int i0) __attribute__((always_inline)) {
+    const int ns = min(7, cnt - i0);
+#pragma unroll
+    for (int k = 0; k < kFixPer; ++k) {
+      const int e = lane + 64 * k;
+      if (e < ns * 363) {
+        const int sl = e / 363, rem = e - 363 * sl, r = rem / 33, f = rem - 33 * r;
+        xw[sl * kFixXFloats + r * kFixXRow + f] = v[k];
+      }
+    }
+  };
+
+  int i0 = wave * 7;
+  if (FIXUP_AB != 2) fetch(i0);
+  for (; i0 < cnt; i0 += kFixWaves * 7) {
+    const int ns = min(7, cnt - i0);  // entries of this pass (uniform)
+    if (FIXUP_AB != 2) store(i0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    if (FIXUP_AB != 2) fetch(i0 + kFixWaves * 7);  // the next pass's windows in flight
+    const bool act = slot < ns;
+    const uint32_t ent = act ? entry(i0 + slot) : 0u;
+    uint32_t m = ent & 15u;
+    const uint32_t pq = ent >> 4;
+    const int pp = (int)(pq >> 4);  // pool pixel (< 2^24)
+    const int64_t p = pp;
+    const int cq = (int)(pq & 15u);
+    const int px = pp % a.Wo;
+    const int py = (pp / a.Wo) % a.Ho;
+    const int oy = 2 * py - 1 + dy, ox = 2 * px - 1 + dx;
+    const bool valid = act && oy >= 0 && oy < Hc && ox >= 0 && ox < Wc;
+    // this position's window: rows 2 dy .. 2 dy + 6, floats 6 dx .. 6 dx + 20 of each
+    const float* xr = xw + (act ? slot : 0) * kFixXFloats + 2 * dy * kFixXRow + 6 * dx;
+    while (__ballot(m != 0u)) {  // the wave's entries, one channel each round
+      const bool has = m != 0u;
+      const int c = 4 * cq + (has ? __builtin_ctz(m) : 0);
+      m &= m - 1u;
+      const float* wc = wl + c * 7 * kFixWRow;
+      double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll 1
+      for (int ky = 0; ky < (FIXUP_AB == 1 ? 0 : 7); ++ky) {
+        const float* xk = xr + ky * kFixXRow;
+        const float* wk = wc + ky * kFixWRow;
+#pragma unroll
+        for (int k = 0; k < 20; k += 2) {
+          const float2 xv = *reinterpret_cast<const float2*>(xk + k);
+          const float2 wv = *reinterpret_cast<const float2*>(wk + k);
+          acc0 = fma((double)xv.x, (double)wv.x, acc0);
+          acc1 = fma((double)xv.y, (double)wv.y, acc1);
+        }
+        acc0 = fma((double)xk[20], (double)wk[20], acc0);
+      }
+      const double acc = acc0 + acc1;
+      float vv = (has && valid) ? (float)(__builtin_signbit(a.scale[c]) ? -acc : acc)
+                                : -__builtin_inff();
+      // window max on lane 9 slot (the shuffles read lanes of the same slot; lane 63's
+      // reads wrap and are unused)
+      float vm = vv;
+#pragma unroll
+      for (int jj = 1; jj < 9; ++jj) vm = fmaxf(vm, __shfl(vv, lane + jj));
+      if (has && j == 0) {
+        const float y = fmaxf(fmaf(vm, fabsf(a.scale[c]), a.shift[c]), 0.0f);
+        a.out[p * 64 + c] = y;
+        if (a.codes_a)
+          a.codes_a[p * a.cp_a + c] =
+              (int16_t)code_bits(tr_value_g1_inv(y, a.inv_a, a.maxv_a, a.k_a), a.fmt_a);
+        if (a.codes_b)
+          a.codes_b[p * a.cp_b + c] =
+              (int16_t)code_bits(tr_value_g1_inv(y, a.inv_b, a.maxv_b, a.k_b), a.fmt_b);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this pass's window reads are done
+    __builtin_amdgcn_wave_barrier();     // before the next pass restages the windows
+  }
+}
+
+__global__ __launch_bounds__(kFixThreads) void stem_fixup_kernel(PoolArgs a, int tp,
+                                                                 int tiles) {
+  extern __shared__ __attribute__((aligned(16))) float fix_lds[];
+  const int g = blockIdx.x;
+  const int t_begin = (int)((int64_t)g * tiles / gridDim.x);
+  stem_fixup_run(a, a.fix_list + (int64_t)t_begin * tp * a.Wo * 16, (int)a.fix_counts[g],
+                 fix_lds);
+}
+static_assert(kFixThreads == kStemThreads && kFixLds <= kStemDynLds,
+              "the fix-up runs as the stem kernel's tail phase in its workgroup and LDS");
 
 // FIX: the exact fix-up's listing (a.fix_list): each conv output's input-window norm is summed
 // beside its MFMAs, pooled like the values, and bounds the split conv's error.
@@ -666,172 +842,11 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
     prev_kx = kx;
   }
   if (fix) {
-    __syncthreads();
+    __syncthreads();  // (also: every output store of the workgroup has completed)
     if (tid == 0) a.fix_counts[blockIdx.x] = fix_n;
-  }
-}
-
-// Exact fix-up of the listed outputs (one launch after the stem, same stream).  Each entry
-// names a pool pixel p and a 4-bit mask of channels in quad cq; for each such channel the
-// nine conv outputs of its pool window are recomputed exactly -- fp32 x times fp32 w is exact
-// in fp64 and a 147-term fp64 sum is within 2^-46 of its magnitude sum, then one rounding to
-// fp32 -- and the pooled value goes through the same BN fma, ReLU and code path as the
-// stem's epilogue.  Workgroup g walks the entries of stem workgroup g's segment, 7 per wave
-// and pass: the wave stages the 7 pool windows' 11 x 11 x 3 input values in LDS (one
-// coalesced sweep), then lane 9 slot + j computes window position j from LDS (weights staged
-// once per workgroup, fp32 [64][7][22], rows padded for 8-byte pairs), and the slot's max is
-// gathered by lane shuffles.
-__device__ float g_fix_zero[4];  // static storage: zeros, never written
-constexpr int kFixWaves = 8;
-constexpr int kFixThreads = 64 * kFixWaves;
-constexpr int kFixWRow = 22;                       // floats per weight kernel row (21 + pad)
-constexpr int kFixWFloats = 64 * 7 * kFixWRow;     // 9856
-constexpr int kFixXRow = 34;                       // floats per window row (33 + pad)
-constexpr int kFixXFloats = 11 * kFixXRow;         // per slot
-constexpr int kFixEnts = 4096;                     // entries staged in LDS (more: read global)
-constexpr int kFixLds = (kFixWFloats + kFixWaves * 7 * kFixXFloats + kFixEnts + kFixWaves * 32) * 4;
-
-__global__ __launch_bounds__(kFixThreads) void stem_fixup_kernel(PoolArgs a, int tp,
-                                                                 int tiles) {
-  extern __shared__ __attribute__((aligned(16))) float fix_lds[];
-  float* wl = fix_lds;
-  uint32_t* ents = reinterpret_cast<uint32_t*>(fix_lds + kFixWFloats + kFixWaves * 7 * kFixXFloats);
-  const int g = blockIdx.x;
-  const int t_begin = (int)((int64_t)g * tiles / gridDim.x);
-  const uint32_t* seg = a.fix_list + (int64_t)t_begin * tp * a.Wo * 16;
-  const int cnt = (int)a.fix_counts[g];
-  if (cnt == 0) return;  // (uniform: before the barrier)
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  float* xw = fix_lds + kFixWFloats + wave * 7 * kFixXFloats;
-  // weights [c][ky][kx * 3 + ci] from w64 (exact in fp32: they are the fp32 weights), and
-  // the segment's entries
-  for (int i = tid; i < 64 * 147; i += kFixThreads) {
-    const int c = i / 147, k = i - c * 147, ky = k / 21;
-    wl[c * 7 * kFixWRow + ky * kFixWRow + (k - ky * 21)] = (float)a.w64[i];
-  }
-  for (int i = tid; i < cnt && i < kFixEnts; i += kFixThreads) ents[i] = seg[i];
-  __syncthreads();
-  if (FIXUP_AB == 3) return;
-  auto entry = [&](int i) __attribute__((always_inline)) {
-    return i < kFixEnts ? ents[i] : seg[i];
-  };
-  const int slot = lane / 9;
-  const int j = lane - 9 * slot;
-  const int dy = j / 3, dx = j - 3 * (j / 3);
-  const int Hc = a.H / 2, Wc = a.W / 2;
-
-  // The pool windows of pass i0 (input rows 4 py - 5 .. 4 py + 5, columns 4 px - 5 .. 4 px +
-  // 5, 363 values each): value e of the pass -> slot e / 363, row, float, so consecutive
-  // lanes load consecutive floats of one input row (a wave instruction touches a few cache
-  // lines); every lane issues its 40 loads with no branch around a load (positions outside
-  // the image read the zero page).  Software-pipelined: a pass's loads are issued before the
-  // previous pass computes.  Per slot and pass: [iy0, ix0, element offset of (iy0, ix0)]
-  // in the wave's LDS scratch (decoded once by lanes 0..6).
-  int* sinfo = reinterpret_cast<int*>(ents + kFixEnts) + wave * 32;
-  constexpr int kFixPer = (7 * 363 + 63) / 64;  // 40 values per lane
-  float v[kFixPer];
-  auto fetch = [&](int i0) __attribute__((always_inline)) {
-    const int ns = i0 < cnt ? min(7, cnt - i0) : 0;
-    if (lane < ns) {
-      const int pp = (int)(entry(i0 + lane) >> 8);  // pool pixel (< 2^24)
-      const int px = pp % a.Wo;
-      const int t = pp / a.Wo;
-      const int py = t % a.Ho, n = t / a.Ho;
-      sinfo[4 * lane] = 4 * py - 5;
-      sinfo[4 * lane + 1] = 4 * px - 5;
-      sinfo[4 * lane + 2] = n;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < kFixPer; ++k) {
-      const int e = lane + 64 * k;
-      const bool live = e < ns * 363;
-      const int sl = live ? e / 363 : 0;
-      const int rem = e - 363 * sl, r = rem / 33, f = rem - 33 * r;
-      const int iy = sinfo[4 * sl] + r, ix = sinfo[4 * sl + 1] + f / 3;
-      const bool ok = live && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      const float* sp =
-          ok ? a.x + (((int64_t)sinfo[4 * sl + 2] * a.H + iy) * a.W + ix) * 3 + (f - 3 * (f / 3))
-             : g_fix_zero;
-      v[k] = *sp;
-    }
-  };
-  auto store = [&](int i0) __attribute__((always_inline)) {
-    const int ns = min(7, cnt - i0);
-#pragma unroll
-    for (int k = 0; k < kFixPer; ++k) {
-      const int e = lane + 64 * k;
-      if (e < ns * 363) {
-        const int sl = e / 363, rem = e - 363 * sl, r = rem / 33, f = rem - 33 * r;
-        xw[sl * kFixXFloats + r * kFixXRow + f] = v[k];
-      }
-    }
-  };
-
-  int i0 = wave * 7;
-  if (FIXUP_AB != 2) fetch(i0);
-  for (; i0 < cnt; i0 += kFixWaves * 7) {
-    const int ns = min(7, cnt - i0);  // entries of this pass (uniform)
-    if (FIXUP_AB != 2) store(i0);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    if (FIXUP_AB != 2) fetch(i0 + kFixWaves * 7);  // the next pass's windows in flight
-    const bool act = slot < ns;
-    const uint32_t ent = act ? entry(i0 + slot) : 0u;
-    uint32_t m = ent & 15u;
-    const uint32_t pq = ent >> 4;
-    const int pp = (int)(pq >> 4);  // pool pixel (< 2^24)
-    const int64_t p = pp;
-    const int cq = (int)(pq & 15u);
-    const int px = pp % a.Wo;
-    const int py = (pp / a.Wo) % a.Ho;
-    const int oy = 2 * py - 1 + dy, ox = 2 * px - 1 + dx;
-    const bool valid = act && oy >= 0 && oy < Hc && ox >= 0 && ox < Wc;
-    // this position's window: rows 2 dy .. 2 dy + 6, floats 6 dx .. 6 dx + 20 of each
-    const float* xr = xw + (act ? slot : 0) * kFixXFloats + 2 * dy * kFixXRow + 6 * dx;
-    while (__ballot(m != 0u)) {  // the wave's entries, one channel each round
-      const bool has = m != 0u;
-      const int c = 4 * cq + (has ? __builtin_ctz(m) : 0);
-      m &= m - 1u;
-      const float* wc = wl + c * 7 * kFixWRow;
-      double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll 1
-      for (int ky = 0; ky < (FIXUP_AB == 1 ? 0 : 7); ++ky) {
-        const float* xk = xr + ky * kFixXRow;
-        const float* wk = wc + ky * kFixWRow;
-#pragma unroll
-        for (int k = 0; k < 20; k += 2) {
-          const float2 xv = *reinterpret_cast<const float2*>(xk + k);
-          const float2 wv = *reinterpret_cast<const float2*>(wk + k);
-          acc0 = fma((double)xv.x, (double)wv.x, acc0);
-          acc1 = fma((double)xv.y, (double)wv.y, acc1);
-        }
-        acc0 = fma((double)xk[20], (double)wk[20], acc0);
-      }
-      const double acc = acc0 + acc1;
-      float vv = (has && valid) ? (float)(__builtin_signbit(a.scale[c]) ? -acc : acc)
-                                : -__builtin_inff();
-      // window max on lane 9 slot (the shuffles read lanes of the same slot; lane 63's
-      // reads wrap and are unused)
-      float vm = vv;
-#pragma unroll
-      for (int jj = 1; jj < 9; ++jj) vm = fmaxf(vm, __shfl(vv, lane + jj));
-      if (has && j == 0) {
-        const float y = fmaxf(fmaf(vm, fabsf(a.scale[c]), a.shift[c]), 0.0f);
-        a.out[p * 64 + c] = y;
-        if (a.codes_a)
-          a.codes_a[p * a.cp_a + c] =
-              (int16_t)code_bits(tr_value_g1_inv(y, a.inv_a, a.maxv_a, a.k_a), a.fmt_a);
-        if (a.codes_b)
-          a.codes_b[p * a.cp_b + c] =
-              (int16_t)code_bits(tr_value_g1_inv(y, a.inv_b, a.maxv_b, a.k_b), a.fmt_b);
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this pass's window reads are done
-    __builtin_amdgcn_wave_barrier();     // before the next pass restages the windows
+    // the workgroup's own segment, right after its last tile: no second launch, and the
+    // workgroups that finish early overlap it with the others' tiles
+    if (FIX_FUSED) stem_fixup_run(a, fix_seg, (int)fix_n, reinterpret_cast<float*>(lds_raw));
   }
 }
 
@@ -855,7 +870,7 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
     hipError_t e = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&stem_conv_pool_kernel<TP, QMAX, ONE, FIX>),
         hipFuncAttributeMaxDynamicSharedMemorySize, kStemDynLds);
-    if (e == hipSuccess && FIX)
+    if (e == hipSuccess && FIX && !FIX_FUSED)
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_fixup_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kFixLds);
     if (e != hipSuccess) return e;
@@ -869,9 +884,12 @@ hipError_t launch_stem_one(const PoolArgs& a, hipStream_t stream) {
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return hipSuccess;
   if (a.fix_list && grid * 4 > kStemFixCountsBytes) return hipErrorInvalidValue;
+  // the fix-up tail phase reuses the dynamic LDS with its own layout (LDS past the launch's
+  // allocation is not the workgroup's: writes there are dropped, reads return zero)
+  if (FIX && FIX_FUSED && bytes < kFixLds) bytes = kFixLds;
   stem_conv_pool_kernel<TP, QMAX, ONE, FIX>
       <<<dim3(grid), kStemThreads, (size_t)bytes, stream>>>(b, sc, nb, tiles);
-  if (FIX) {
+  if (FIX && !FIX_FUSED) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     stem_fixup_kernel<<<dim3(grid), kFixThreads, kFixLds, stream>>>(b, TP, tiles);
