@@ -61,7 +61,10 @@
 #define STEM_PF 0  // 1: the next K-step's input slices read during this step's MFMAs
 #endif
 #ifndef STEM_NRM_MFMA
-#define STEM_NRM_MFMA 1  // window norms: 1 the diagonal of an MFMA, 0 v_dot2 on the VALU
+#define STEM_NRM_MFMA 0  // window norms: 1 the diagonal of an MFMA, 0 v_dot2 on the VALU
+                         // (r06: with the fix-up as the tail phase the VALU form is 12-14 us
+                         // faster per 256-image call, equal in the two-chunk bench;
+                         // profiles/r06_fixup_ab.txt)
 #endif
 #ifndef STEM_QF32
 #define STEM_QF32 0  // 1: the code-table index from an fp32 product (exact fp64 quotient only
