@@ -1,5 +1,5 @@
 # Exact-stem A/B: in-tree build vs lib/libtq_hip_sepfix.so (built with the option under test:
-# first FIX_FUSED=0, then STEM_NRM_MFMA=1): exact-mode tests, stem call times, then interleaved
+# FIX_FUSED=0, STEM_NRM_MFMA=1, a two-ahead fetch in turn): exact-mode tests, stem call times, then interleaved
 # bench runs with the exact stem.
 set -u
 O=gpurun_out/fixfused_ab; mkdir -p $O
