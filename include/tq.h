@@ -363,14 +363,16 @@ int tq_bn_relu_maxpool_encode(const float *x, int64_t n, int64_t h, int64_t w, i
  *            pack_stem_weight)
  *   out      fp32 [n][h/4][w/4][64] (ho = h/4, wo = w/4)
  * Exact fix-up (w64, wbound, workspace all non-NULL; all NULL = the split conv's result
- * stands): the split conv of output channel c is within wbound[c] * M of the exact sum (M
- * the max |x| of the input rows the kernel staged for it).  Every output whose quotient
- * out / sf lies within that error (through BN) of a rounding midpoint is listed in the
- * workspace and recomputed by a second kernel on the same stream from the fp64 weights --
- * exact products, fp64 sum, one rounding to fp32 -- so every code equals the code of the
- * correctly rounded fp32 conv followed by the same BN / ReLU / max-pool.
+ * stands): the split conv of output channel c at a conv position is within wbound[c] * |x|
+ * of the exact sum (|x| the 2-norm of the position's 7x7x3 input window, summed by the
+ * kernel beside its MFMAs; Cauchy-Schwarz).  Every pooled output whose quotient out / sf lies
+ * within that error (through BN) of a rounding midpoint is listed in the workspace and
+ * recomputed from the fp64 weights by the same launch (each workgroup's tail phase, after its
+ * last tile) -- exact products, fp64 sum, one rounding to fp32 -- so every code equals the
+ * code of the correctly rounded fp32 conv followed by the same BN / ReLU / max-pool.  The
+ * workspace's first 4096 bytes hold the per-workgroup counts of listed outputs (uint32).
  *   w64      fp64 [64][7][7][3] conv weights (kernel row, column, input channel)
- *   wbound   fp32 [64], >= the split conv's relative error bound times sum |w[c]|
+ *   wbound   fp32 [64], >= the split conv's relative error bound times |w[c]|_2
  *            (tq_ops.pack_stem_exact)
  *   workspace  >= tq_stem_workspace_bytes(n, h, w) bytes, 16-byte aligned; needs
  *            n * ho * wo < 2^24
