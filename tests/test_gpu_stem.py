@@ -145,7 +145,7 @@ def _exact_codes(x, wt, sc, sh, quant):
     return pooled, np.rint(yq.reshape(pooled.shape) / np.float32(sf)).astype(np.int64)
 
 
-def _exact_case(n, h, w, fmt, xs, seed, quant, scale_bands=False):
+def _exact_case(n, h, w, fmt, xs, seed, quant, scale_bands=False, workspace=None):
     sf, bw, dt = quant
     torch.manual_seed(seed)
     x = torch.randn(n, 3, h, w) * xs
@@ -164,7 +164,8 @@ def _exact_case(n, h, w, fmt, xs, seed, quant, scale_bands=False):
     wsplit = tq_ops.pack_stem_weight(wt.to(DEV))
     exact = tq_ops.pack_stem_exact(wt.to(DEV))
     tq_native.stem_conv_pool_encode(x.to(DEV), wsplit, sc.to(DEV), sh.to(DEV), out,
-                                    codes_a=codes, quant_a=quant, exact=exact)
+                                    codes_a=codes, quant_a=quant, exact=exact,
+                                    workspace=workspace)
     codes_split = torch.zeros_like(codes)
     out_split = torch.empty_like(out)
     tq_native.stem_conv_pool_encode(x.to(DEV), wsplit, sc.to(DEV), sh.to(DEV), out_split,
@@ -213,6 +214,22 @@ def test_stem_exact_fixup_random_sweep(seed):
              int(rng.integers(1, 5)))
     _exact_case(int(rng.integers(1, 4)), h, w, fmt, xs, 7000 + seed, quant,
                 bool(rng.random() < 0.5))
+
+
+def test_stem_exact_fixup_long_segments():
+    """Workgroup segments longer than the fix-up's LDS entry stage (4096 entries; the rest are
+    read from the workspace in global memory): 300 images of 16 x 336 (300 tiles over <= 256
+    workgroups, so some take two tiles of 4 x 84 pool pixels x 16 channel quads), and an sf
+    / bitwidth at which the error bound covers a large part of every quotient's unit interval
+    (most quads listed).  Every code is still the correctly rounded conv's."""
+    n, h, w = 300, 16, 336
+    ws = tq_native.stem_workspace(n, h, w, DEV).zero_()  # (counts past the grid stay 0)
+    _, touched, total = _exact_case(n, h, w, torch.int16, 1.0, 4242, (1e-4, 14, 3),
+                                    workspace=ws)
+    counts = ws[:4096].view(torch.int32).cpu().numpy()
+    assert counts.max() > 4096, int(counts.max())
+    print("long segments: max %d entries per workgroup, %d listed in all, %d outputs changed "
+          "of %d" % (int(counts.max()), int(counts.sum()), touched, total))
 
 
 def test_stem_exact_rejects_partial_args():
