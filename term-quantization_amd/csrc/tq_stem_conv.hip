@@ -322,6 +322,7 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   __shared__ uint32_t tile_max[2];  // max |x| (fp32 bits) of a tile's rows, by tile parity
   __shared__ uint32_t fix_n;        // near-midpoint outputs this workgroup listed (fix-up)
   __shared__ float fix_ew[2][64];   // per side and channel: quotient error per unit norm
+  __shared__ float fix_sh[2];       // per side: 2^-23 max |shift| / sf + 2^-30 (flag slack)
   __shared__ float fix_nrm[8][8];   // per wave: pooled window norms^2 of the strip's 7 pixels
   uint16_t* ws = reinterpret_cast<uint16_t*>(lds_raw);
   float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(lds_raw) + kStemWBytes);
@@ -373,8 +374,13 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
   constexpr bool fix = FIX;
   if (fix && tid < 128) {  // visible after the first barrier
     const int c = tid & 63;
+    const float inv = (float)(tid < 64 ? a.inv_a : a.inv_b);
     const float wb = a.wbound[c] * fabsf(a.scale[c]) * 1.00390625f;
-    fix_ew[tid >> 6][c] = wb * (float)(tid < 64 ? a.inv_a : a.inv_b);
+    fix_ew[tid >> 6][c] = wb * inv;
+    float sh = fabsf(a.shift[c]) * inv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sh = fmaxf(sh, __shfl_xor(sh, o));
+    if (c == 0) fix_sh[tid >> 6] = fmaf(sh, 0x1p-23f, 0x1p-30f);
   }
 
   // Input staging, software-pipelined across tiles: the next tile's rows are loaded into
@@ -715,15 +721,23 @@ __global__ __launch_bounds__(kStemThreads, 1) void stem_conv_pool_kernel(PoolArg
               // (+ 0.5 scaled units: the fp16 subnormal remainders of inputs below ~2^-17 of
               // the tile's max, at most 2^-25 each, are not relative to the norm)
               const float wn = (sqrtf(fix_nrm[wave][f >> 4]) + 0.5f) * unscale;
-              // (an fp32 product is within two ulps of the quotient the codes round: inside
-              // the 2^-12 of slack for quotients below 2^10; past the clamp every code is
-              // maxv's, so a flag there is only a harmless recompute)
+              // Rounding slack in quotient units (r = y / sf; codes differ only if the exact
+              // quotients y_split / sf and y_exact / sf straddle a half-integer, and fp32
+              // rounding is monotone): this fp32 product vs y_split / sf <= 2^-23 r (1/sf
+              // rounded to fp32, the product rounded); the BN fma's rounding on either side
+              // <= 2^-23 r together; the correctly rounded conv's own rounding <= 2^-24 |s v|
+              // <= 2^-24 (r + |shift| / sf).  In all 5 * 2^-24 r + 2^-24 |shift| / sf, taken
+              // as 2^-21 r + 2^-23 max|shift| / sf + 2^-30 (fix_sh).  (Before: a flat 2^-12, enough only for
+              // r < ~600 and 2-10x more than needed below ~200.)  Past the clamp every code
+              // is maxv's, so a flag there is only a harmless recompute.
               const float invf = (float)inv;
+              const float shs = fix_sh[side];
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const float r = yv[i] * invf;
+                const float slack = fmaf(r, 0x1p-21f, shs);
                 if (STEM_FIXAB != 2 &&
-                    fabsf(__builtin_amdgcn_fractf(r) - 0.5f) <= fmaf(wn, ew[i], 0x1p-12f))
+                    fabsf(__builtin_amdgcn_fractf(r) - 0.5f) <= fmaf(wn, ew[i], slack))
                   fm |= 1u << i;
               }
               if (fm) ent = ((uint32_t)(p * 16 + (f & 15)) << 4) | (ent & 15u) | fm;

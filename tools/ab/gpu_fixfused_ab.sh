@@ -1,5 +1,6 @@
 # Exact-stem A/B: in-tree build vs lib/libtq_hip_sepfix.so (built with the option under test:
-# FIX_FUSED=0, STEM_NRM_MFMA=1, a two-ahead fetch in turn): exact-mode tests, stem call times, then interleaved
+# FIX_FUSED=0, STEM_NRM_MFMA=1, a two-ahead fetch, the flat 2^-12 flag slack in turn): exact-mode
+# tests, stem call times, then interleaved
 # bench runs with the exact stem.
 set -u
 O=gpurun_out/fixfused_ab; mkdir -p $O
@@ -9,7 +10,7 @@ rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && exit $rc
 for v in new old; do
   L=$PWD/term-quantization_amd/lib/libtq_hip.so; [ $v = old ] && L=$OLD
   TQ_LIB_PATH=$L timeout -k 10 300 python3 tools/ab/stem_fix_count.py 128 256 > $O/count_$v.txt 2>&1
-  rc=$?; echo "== $v"; grep -E "==|us per" $O/count_$v.txt; [ $rc -ne 0 ] && exit $rc
+  rc=$?; echo "== $v"; grep -E "==|listed|us per" $O/count_$v.txt; [ $rc -ne 0 ] && exit $rc
 done
 for r in 1 2 3; do for v in new old; do
   L=$PWD/term-quantization_amd/lib/libtq_hip.so; [ $v = old ] && L=$OLD
