@@ -216,6 +216,17 @@ def test_stem_exact_fixup_random_sweep(seed):
                 bool(rng.random() < 0.5))
 
 
+@pytest.mark.parametrize("fmt", [torch.float16, torch.int16])
+def test_stem_exact_fixup_large_quotients(fmt):
+    """11-bit codes with quotients up to ~2000 (sf 0.0015 on N(0, 1) inputs): the listing's
+    rounding slack grows with the quotient (2^-21 r + 2^-23 max|shift| / sf), where a flat
+    slack stops covering the fp32 rounding terms (r above ~600).  Every code is the correctly
+    rounded conv's."""
+    flips_split, touched, total = _exact_case(6, 224, 224, fmt, 1.0, 4711, (0.0015, 11, 3))
+    print("large quotients: split-only flips %d, fixed-up outputs %d of %d"
+          % (flips_split, touched, total))
+
+
 def test_stem_exact_fixup_long_segments():
     """Workgroup segments longer than the fix-up's LDS entry stage (4096 entries; the rest are
     read from the workspace in global memory): 300 images of 16 x 336 (300 tiles over <= 256
